@@ -1,0 +1,34 @@
+// hwy_internal.h -- launch parameters shared by hwy_api.cpp (host) and hwy_kernels.hip.
+#ifndef HWY_INTERNAL_H_
+#define HWY_INTERNAL_H_
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hwy.h"
+
+struct StepParams {
+  hwy_config cfg;
+  uint32_t* state;
+  const float* actions;
+  float* obs;
+  float* reward;
+  uint8_t* term;
+  uint8_t* trunc;
+  float* ep_ret;
+  int32_t* ep_len;
+  const float* pe_table;
+  const uint64_t* seeds;
+  const uint8_t* mask;
+  int fout;
+};
+
+extern "C" {
+int hwy_launch_step(const StepParams* p, hipStream_t s);
+int hwy_launch_reset(const StepParams* p, hipStream_t s);
+int hwy_launch_obs_pe(const float* in, float* out, int E, int N, int F, int kind, int d, int ego,
+                      float max_dist, const float* table, const float* dov, hipStream_t s);
+int hwy_launch_gae(const float* rew, const uint8_t* done, const float* val, const float* last_val,
+                   double gamma, double lam, int T, int E, float* adv, float* ret, hipStream_t s);
+int hwy_launch_math(int op, const float* in, const float* in2, float* out, int n, hipStream_t s);
+}
+#endif

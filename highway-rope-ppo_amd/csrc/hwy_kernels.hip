@@ -1,0 +1,906 @@
+// hwy_kernels.hip -- gfx950 kernels of the vectorised highway-v0 hot path.
+//
+// Layout: one 64-lane wavefront per env, lane v = vehicle v of road.vehicles (v = 0 ego,
+// 1..vehicles_count IDM traffic).  A 256-thread workgroup advances 4 envs.  The per-env state is
+// field-major SoA in HBM ([field][env][64] u32, include/hwy.h) so each wave loads 256
+// contiguous bytes per field once, runs all sim_freq/policy_freq frames in registers, and
+// stores once.  Cross-vehicle reads use v_readlane (uniform index, SGPR broadcast) or
+// ds_bpermute (per-lane index); nothing else touches LDS except the observation row maps.
+//
+// Semantics follow upstream highway-env 1.10.1 as restated in oracle/hwy_oracle.c, which runs
+// every vehicle sequentially; the parallel formulation below is arranged to give the same bits:
+//   * Road.act order dependence: MOBIL decisions do not read other vehicles' target lanes, so
+//     they run in parallel; the "abort ongoing lane change" check (which does) runs afterwards
+//     over the mid-change vehicles in ascending index, each seeing the already-final targets of
+//     lower-index vehicles and the frame-start targets of higher-index ones.
+//   * Road.step collisions: lane k evaluates every pair {k, j} (always as a = lower index, so
+//     both lanes of a pair compute identical bits) in ascending j, which is exactly the order
+//     in which upstream's i<j double loop last writes k's impact.
+// All floating point goes through hwy_math.h and is compiled with -ffp-contract=off.
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "hwy.h"
+#include "hwy_math.h"
+#include "hwy_internal.h"
+
+#define WAVE 64
+#define ENVS_PER_BLOCK 4
+
+// upstream constants (same literals as oracle/hwy_oracle.c)
+#define LANE_WIDTH 4.0f
+#define LANE_VEH_LEN 5.0f
+#define ROAD_LENGTH 10000.0f
+#define VEH_LENGTH 5.0f
+#define VEH_WIDTH 2.0f
+#define MAX_SPEED 40.0f
+#define MIN_SPEED (-40.0f)
+#define KP_HEADING (1.0f / 0.2f)
+#define KP_LATERAL (1.0f / 0.6f)
+#define MAX_STEERING (HM_PI_F / 3.0f)
+#define ACC_MAX 6.0f
+#define COMFORT_ACC_MAX 3.0f
+#define DISTANCE_WANTED 10.0f
+#define TIME_WANTED 1.5f
+#define LANE_CHANGE_MIN_ACC_GAIN 0.2f
+#define LANE_CHANGE_MAX_BRAKING_IMPOSED 2.0f
+#define LANE_CHANGE_DELAY 1.0f
+#define PERCEPTION_DISTANCE 200.0f
+#define TWO_SQRT_AB 7.745966692414834f
+#define VEH_DIAGONAL 5.385164807134504f
+
+// ------------------------------------------------------------------------- wave primitives
+__device__ __forceinline__ float rdlf(float v, int k) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
+}
+__device__ __forceinline__ int rdli(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
+// per-lane gather; must run with all 64 lanes active
+__device__ __forceinline__ float shf(float v, int src) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
+}
+__device__ __forceinline__ int shi(int v, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
+__device__ __forceinline__ uint64_t ballot(bool p) { return (uint64_t)__ballot(p); }
+__device__ __forceinline__ bool wave_any(bool p) { return ballot(p) != 0ull; }
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ------------------------------------------------------------------------- vehicle state
+struct Veh {
+  float x, y, h, spd, tsp, dlt, tmr, ix, iy;
+  float aacc, asteer;  // Vehicle.action (lane 0: the ego's dict, persists across frames)
+  int ln, tl;
+  bool crashed, imp, present;
+};
+
+__device__ __forceinline__ float lane_lat(float y, int c) { return y - (float)c * LANE_WIDTH; }
+
+__device__ __forceinline__ bool on_lane_m(float x, float y, int c, float margin) {
+  float lat = lane_lat(y, c);
+  return hm_absf(lat) <= LANE_WIDTH / 2.0f + margin && -LANE_VEH_LEN <= x &&
+         x < ROAD_LENGTH + LANE_VEH_LEN;
+}
+
+__device__ __forceinline__ int closest_lane(float y, int lanes) {
+  int best = 0;
+  float bd = hm_absf(lane_lat(y, 0));
+  for (int c = 1; c < lanes; ++c) {
+    float d = hm_absf(lane_lat(y, c));
+    if (d < bd) {
+      bd = d;
+      best = c;
+    }
+  }
+  return best;
+}
+
+// IDMVehicle.desired_gap(ego=a, front=b)
+__device__ __forceinline__ float desired_gap(float a_spd, float a_c, float a_s, float b_spd,
+                                             float b_c, float b_s) {
+  float avx = a_spd * a_c, avy = a_spd * a_s;
+  float bvx = b_spd * b_c, bvy = b_spd * b_s;
+  float dv = (avx - bvx) * a_c + (avy - bvy) * a_s;
+  return (DISTANCE_WANTED + a_spd * TIME_WANTED) + (a_spd * dv) / TWO_SQRT_AB;
+}
+
+// IDMVehicle.acceleration(ego_vehicle=ev, front_vehicle=fv) with the caller's DELTA
+__device__ __forceinline__ float idm_acc(float ev_spd, float ev_tsp, float ev_x, float ev_c,
+                                         float ev_s, bool has_front, float fv_x, float fv_spd,
+                                         float fv_c, float fv_s, float delta, float limit) {
+  float tsp = hm_clipf(ev_tsp, 0.0f, limit);
+  float base = hm_maxf(ev_spd, 0.0f) / hm_absf(hm_not_zero(tsp));
+  float acc = COMFORT_ACC_MAX * (1.0f - hm_powf(base, delta));
+  if (has_front) {
+    float d = fv_x - ev_x;
+    float g = desired_gap(ev_spd, ev_c, ev_s, fv_spd, fv_c, fv_s) / hm_not_zero(d);
+    acc = acc - COMFORT_ACC_MAX * (g * g);
+  }
+  return acc;
+}
+
+// ControlledVehicle.steering_control(target lane c)
+__device__ __forceinline__ float steering_control(float y, float h, float spd, int c) {
+  float lat = lane_lat(y, c);
+  float lane_future_heading = 0.0f;
+  float lateral_speed_command = -KP_LATERAL * lat;
+  float heading_command =
+      hm_asinf(hm_clipf(lateral_speed_command / hm_not_zero(spd), -1.0f, 1.0f));
+  float heading_ref = lane_future_heading + hm_clipf(heading_command, -HM_PIO4_F, HM_PIO4_F);
+  float heading_rate_command = KP_HEADING * hm_wrap_to_pi(heading_ref - h);
+  float slip_angle = hm_asinf(
+      hm_clipf((VEH_LENGTH / 2.0f) / hm_not_zero(spd) * heading_rate_command, -1.0f, 1.0f));
+  float steering_angle = hm_atanf(2.0f * hm_tanf(slip_angle));
+  return hm_clipf(steering_angle, -MAX_STEERING, MAX_STEERING);
+}
+
+// utils.are_polygons_intersecting on the two 5x2 m rectangles (a = lower road index)
+__device__ void sat_collide(float ax, float ay, float ac, float as, float dax, float day, float bx,
+                            float by, float bc, float bs, float dbx, float dby, bool* inter_out,
+                            bool* will_out, float* tx, float* ty) {
+  const float px[4] = {-VEH_LENGTH / 2.0f, -VEH_LENGTH / 2.0f, VEH_LENGTH / 2.0f, VEH_LENGTH / 2.0f};
+  const float py[4] = {-VEH_WIDTH / 2.0f, VEH_WIDTH / 2.0f, VEH_WIDTH / 2.0f, -VEH_WIDTH / 2.0f};
+  float A[5][2], B[5][2];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    A[k][0] = (ac * px[k] - as * py[k]) + ax;
+    A[k][1] = (as * px[k] + ac * py[k]) + ay;
+    B[k][0] = (bc * px[k] - bs * py[k]) + bx;
+    B[k][1] = (bs * px[k] + bc * py[k]) + by;
+  }
+  A[4][0] = A[0][0];
+  A[4][1] = A[0][1];
+  B[4][0] = B[0][0];
+  B[4][1] = B[0][1];
+  float cdx = (((A[0][0] + A[1][0]) + A[2][0]) + A[3][0]) / 4.0f -
+              (((B[0][0] + B[1][0]) + B[2][0]) + B[3][0]) / 4.0f;
+  float cdy = (((A[0][1] + A[1][1]) + A[2][1]) + A[3][1]) / 4.0f -
+              (((B[0][1] + B[1][1]) + B[2][1]) + B[3][1]) / 4.0f;
+  bool inter = true, will = true, stop = false;
+  float min_distance = __builtin_huge_valf(), axx = 0.0f, axy = 0.0f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = e & 3;
+    float q1x = e < 4 ? A[k][0] : B[k][0], q1y = e < 4 ? A[k][1] : B[k][1];
+    float q2x = e < 4 ? A[k + 1][0] : B[k + 1][0], q2y = e < 4 ? A[k + 1][1] : B[k + 1][1];
+    if (k == 0) stop = false;  // upstream's `break` leaves only the inner (edge) loop
+    if (!stop) {
+      float nx = -q2y + q1y;
+      float ny = q2x - q1x;
+      float nn = __builtin_sqrtf(nx * nx + ny * ny);
+      nx = nx / nn;
+      ny = ny / nn;
+      float min_a = 0.0f, max_a = 0.0f, min_b = 0.0f, max_b = 0.0f;
+#pragma unroll
+      for (int p = 0; p < 5; ++p) {
+        float pa = A[p][0] * nx + A[p][1] * ny;
+        float pb = B[p][0] * nx + B[p][1] * ny;
+        if (p == 0 || pa < min_a) min_a = pa;
+        if (p == 0 || pa > max_a) max_a = pa;
+        if (p == 0 || pb < min_b) min_b = pb;
+        if (p == 0 || pb > max_b) max_b = pb;
+      }
+      float id0 = min_a < min_b ? min_b - max_a : min_a - max_b;
+      if (id0 > 0.0f) inter = false;
+      float vp = nx * (dax - dbx) + ny * (day - dby);
+      if (vp < 0.0f)
+        min_a = min_a + vp;
+      else
+        max_a = max_a + vp;
+      float distance = min_a < min_b ? min_b - max_a : min_a - max_b;
+      if (distance > 0.0f) will = false;
+      if (!inter && !will) {
+        stop = true;
+      } else if (hm_absf(distance) < min_distance) {
+        min_distance = hm_absf(distance);
+        if (cdx * nx + cdy * ny > 0.0f) {
+          axx = nx;
+          axy = ny;
+        } else {
+          axx = -nx;
+          axy = -ny;
+        }
+      }
+    }
+  }
+  *inter_out = inter;
+  *will_out = will;
+  *tx = will ? min_distance * axx : 0.0f;
+  *ty = will ? min_distance * axy : 0.0f;
+}
+
+// ------------------------------------------------------------------------- reset
+__device__ __forceinline__ uint64_t schedule_seed(const hwy_config& C, int e, int episode) {
+  return (uint64_t)(C.seed_base + (int64_t)C.env_offset + (int64_t)e + 1 +
+                    C.seed_stride * (int64_t)episode);
+}
+
+// HighwayEnv._create_vehicles via Vehicle.create_random / IDMVehicle.randomize_behavior
+__device__ void reset_wave(const hwy_config& C, int lane, uint64_t seed, Veh& v) {
+  const int V = C.vehicles_count + 1;
+  const int lanes = C.lanes_count;
+  uint32_t k0 = (uint32_t)(seed & 0xffffffffu), k1 = (uint32_t)(seed >> 32);
+  hm_u32x4 u = hm_philox4x32_10((uint32_t)lane, 0u, 0u, 0x52535431u, k0, k1);
+  float fac = hm_expf((-5.0f / 40.0f) * (float)lanes);
+  int ln;
+  float speed, spacing;
+  if (lane == 0) {
+    ln = C.initial_lane_id >= 0 ? C.initial_lane_id : hm_choice(u.v[0], lanes);
+    speed = 25.0f;
+    spacing = C.ego_spacing;
+  } else {
+    ln = hm_choice(u.v[0], lanes);
+    speed = hm_uniform(u.v[1], 0.7f * C.speed_limit, 0.8f * C.speed_limit);
+    spacing = 1.0f / C.vehicles_density;
+  }
+  float default_spacing = 12.0f + 1.0f * speed;
+  float offset = spacing * default_spacing * fac;
+  float inc = offset * hm_uniform(u.v[2], 0.9f, 1.1f);
+  // x0 = max(x of vehicles already on the road) + inc: a sequential chain in road order
+  float mx = 3.0f * rdlf(offset, 0) + rdlf(inc, 0);
+  float x = mx;
+  for (int k = 1; k < V; ++k) {
+    float xk = mx + rdlf(inc, k);
+    if (lane == k) x = xk;
+    if (xk > mx) mx = xk;
+  }
+  v.x = x;
+  v.y = (float)ln * LANE_WIDTH;
+  v.h = 0.0f;
+  v.spd = speed;
+  v.ln = ln;
+  v.tl = ln;
+  v.tsp = speed;
+  v.present = lane < V;
+  v.crashed = false;
+  v.imp = false;
+  v.ix = 0.0f;
+  v.iy = 0.0f;
+  v.aacc = 0.0f;
+  v.asteer = 0.0f;
+  if (lane == 0) {
+    v.dlt = 0.0f;
+    v.tmr = 0.0f;
+  } else {
+    float t = (v.x + v.y) * HM_PI_F;
+    v.tmr = t - hm_floorf(t);
+    v.dlt = hm_uniform(u.v[3], 3.5f, 4.5f);
+  }
+  if (!v.present) {
+    v.x = v.y = v.spd = v.tsp = v.dlt = v.tmr = 0.0f;
+    v.ln = v.tl = 0;
+  }
+}
+
+// ------------------------------------------------------------------------- observation
+__device__ __forceinline__ float feature_value(int fid, float x, float y, float spd, float h,
+                                               float c, float s) {
+  switch (fid) {
+    case HWY_FEAT_PRESENCE: return 1.0f;
+    case HWY_FEAT_X: return x;
+    case HWY_FEAT_Y: return y;
+    case HWY_FEAT_VX: return spd * c;
+    case HWY_FEAT_VY: return spd * s;
+    case HWY_FEAT_COS_H: return c;
+    case HWY_FEAT_SIN_H: return s;
+    case HWY_FEAT_HEADING: return h;
+  }
+  return 0.0f;
+}
+__device__ __forceinline__ bool is_relative_feature(int fid) {
+  return fid == HWY_FEAT_X || fid == HWY_FEAT_Y || fid == HWY_FEAT_VX || fid == HWY_FEAT_VY;
+}
+
+// One wrapped observation row: in[F] (row values), exy = ego row's first two values.
+// Writes F_out values to out (global).  rope_embed.py:44-74 / dist_embed.py:76-96 /
+// rank_embed.py:45-51.
+__device__ __forceinline__ void write_pe_row(const float* vals, int F, int kind, int d, int row,
+                                             float ex0, float ex1, float max_dist,
+                                             const float* table, bool have_override,
+                                             float override_nd, float* out) {
+  if (kind == HWY_PE_ROPE) {
+    float rx = vals[0] - ex0, ry = vals[1] - ex1;
+    float nd = have_override ? override_nd
+                             : hm_clipf(__builtin_sqrtf(rx * rx + ry * ry) / max_dist, 0.0f, 1.0f);
+#pragma unroll
+    for (int f = 0; f < HWY_MAX_FEATURES; ++f)
+      if (f < F) {
+        if (f < (d & ~1)) {
+          const int p = f >> 1;
+          float th = (HM_TWO_PI_F * nd) * table[p];
+          float s = hm_sinf(th), c = hm_cosf(th);
+          float xx = vals[2 * p], yy = vals[2 * p + 1];
+          out[f] = (f & 1) ? (xx * s + yy * c) : (xx * c - yy * s);
+        } else {
+          out[f] = vals[f];
+        }
+      }
+    return;
+  }
+#pragma unroll
+  for (int f = 0; f < HWY_MAX_FEATURES; ++f)
+    if (f < F) out[f] = vals[f];
+  if (kind == HWY_PE_RANK) {
+    for (int k = 0; k < d; ++k) out[F + k] = table[row * d + k];
+  } else if (kind == HWY_PE_DIST) {
+    float rx = vals[0] - ex0, ry = vals[1] - ex1;
+    float nd = have_override ? override_nd
+                             : hm_clipf(__builtin_sqrtf(rx * rx + ry * ry) / max_dist, 0.0f, 1.0f);
+    const int hd = d / 2;
+    for (int k = 0; k < hd; ++k) {
+      float ang = (HM_TWO_PI_F * nd) * table[k];
+      out[F + k] = hm_sinf(ang);
+      out[F + hd + k] = hm_cosf(ang);
+    }
+  }
+}
+
+// KinematicObservation.observe + fused wrapper for the env of this wave.
+__device__ void observe_wave(const hwy_config& C, int lane, const Veh& v, int step, uint64_t seed,
+                             const float* pe_table, float* obs_env, int fout, int* lds_vor,
+                             int* lds_inv) {
+  const int V = C.vehicles_count + 1;
+  const int N = C.obs_vehicles, F = C.n_features;
+  const float ch = hm_cosf(v.h), sh = hm_sinf(v.h);
+  const float ex = rdlf(v.x, 0), ey = rdlf(v.y, 0), eh = rdlf(v.h, 0), espd = rdlf(v.spd, 0);
+  const float ec = rdlf(ch, 0), es = rdlf(sh, 0);
+  // Road.close_objects_to(ego, PERCEPTION_DISTANCE, count=N-1, see_behind, sort)
+  float dx = v.x - ex, dy = v.y - ey;
+  bool elig = v.present && lane >= 1 && lane < V &&
+              (__builtin_sqrtf(dx * dx + dy * dy) < PERCEPTION_DISTANCE) &&
+              (C.see_behind || -2.0f * VEH_LENGTH < v.x - ex);
+  const uint64_t em = ballot(elig);
+  int rank;
+  if (C.order == HWY_ORDER_SORTED) {
+    float key = hm_absf(v.x - ex);
+    rank = 0;
+    for (int k = 1; k < V; ++k) {
+      if (!((em >> k) & 1ull)) continue;
+      float kk = rdlf(key, k);
+      if (kk < key || (kk == key && k < lane)) ++rank;
+    }
+  } else {
+    rank = __popcll(em & ((1ull << lane) - 1ull));
+  }
+  int nvis = __popcll(em);
+  if (nvis > N - 1) nvis = N - 1;
+  if (elig && rank < N - 1) lds_vor[rank] = lane;
+  // np_random.shuffle(obs[1:]) -> Philox keyed permutation of the N-1 rows
+  const bool shuffle = C.order == HWY_ORDER_SHUFFLED && N > 2;
+  if (shuffle) {
+    uint32_t key = 0u;
+    if (lane < N - 1)
+      key = hm_philox4x32_10((uint32_t)lane, (uint32_t)step, 0u, 0x53485546u,
+                             (uint32_t)(seed & 0xffffffffu), (uint32_t)(seed >> 32))
+                .v[0];
+    int dest = 0;
+    for (int p = 0; p < N - 1; ++p) {
+      uint32_t kp = (uint32_t)rdli((int)key, p);
+      if (kp < key || (kp == key && p < lane)) ++dest;
+    }
+    if (lane < N - 1) lds_inv[dest] = lane;
+  }
+  wave_lds_sync();
+  // output row r = lane
+  int kind = 0;  // 0 zero row, 1 ego, 2 other
+  int src = 0;
+  if (lane == 0) {
+    kind = 1;
+  } else if (lane < N) {
+    int q = shuffle ? lds_inv[lane - 1] : lane - 1;
+    if (q < nvis) {
+      kind = 2;
+      src = lds_vor[q];
+    }
+  }
+  wave_lds_sync();
+  const float sx = shf(v.x, src), sy = shf(v.y, src), sspd = shf(v.spd, src), shh = shf(v.h, src);
+  const float sc = shf(ch, src), ss = shf(sh, src);
+  float vals[HWY_MAX_FEATURES];
+#pragma unroll
+  for (int f = 0; f < HWY_MAX_FEATURES; ++f) {
+    float val = 0.0f;
+    if (f < F && kind != 0) {
+      int fid = C.feature_ids[f];
+      val = feature_value(fid, sx, sy, sspd, shh, sc, ss);
+      if (kind == 2 && !C.absolute && is_relative_feature(fid))
+        val = val - feature_value(fid, ex, ey, espd, eh, ec, es);
+      if (C.normalize && C.has_range[f]) {
+        val = hm_lmap(val, C.features_range[f][0], C.features_range[f][1], -1.0f, 1.0f);
+        if (C.clip) val = hm_clipf(val, -1.0f, 1.0f);
+      }
+    }
+    vals[f] = val;
+  }
+  const int eg = C.ego_idx;
+  const float ex0 = rdlf(vals[0], eg), ex1 = rdlf(vals[1], eg);
+  if (lane < N)
+    write_pe_row(vals, F, C.pe_kind, C.d_embed, lane, ex0, ex1, C.pe_max_dist, pe_table, false,
+                 0.0f, obs_env + (size_t)lane * fout);
+}
+
+// ------------------------------------------------------------------------- state I/O
+__device__ __forceinline__ void load_veh(const uint32_t* st, size_t fstride, size_t idx, int lane,
+                                         int V, Veh& v) {
+  v.x = hm_bits2f(st[HWY_F_X * fstride + idx]);
+  v.y = hm_bits2f(st[HWY_F_Y * fstride + idx]);
+  v.h = hm_bits2f(st[HWY_F_HEADING * fstride + idx]);
+  v.spd = hm_bits2f(st[HWY_F_SPEED * fstride + idx]);
+  v.tsp = hm_bits2f(st[HWY_F_TSPEED * fstride + idx]);
+  v.dlt = hm_bits2f(st[HWY_F_DELTA * fstride + idx]);
+  v.tmr = hm_bits2f(st[HWY_F_TIMER * fstride + idx]);
+  v.ix = hm_bits2f(st[HWY_F_IMPX * fstride + idx]);
+  v.iy = hm_bits2f(st[HWY_F_IMPY * fstride + idx]);
+  v.ln = (int)st[HWY_F_LANE * fstride + idx];
+  v.tl = (int)st[HWY_F_TLANE * fstride + idx];
+  uint32_t fl = st[HWY_F_FLAGS * fstride + idx];
+  v.crashed = (fl & HWY_FLAG_CRASHED) != 0u;
+  v.imp = (fl & HWY_FLAG_IMPACT) != 0u;
+  v.present = ((fl & HWY_FLAG_PRESENT) != 0u) && lane < V;
+  v.aacc = 0.0f;
+  v.asteer = 0.0f;
+}
+
+__device__ __forceinline__ void store_veh(uint32_t* st, size_t fstride, size_t idx, int lane, int V,
+                                          const Veh& v) {
+  const bool live = lane < V;
+  st[HWY_F_X * fstride + idx] = live ? hm_f2bits(v.x) : 0u;
+  st[HWY_F_Y * fstride + idx] = live ? hm_f2bits(v.y) : 0u;
+  st[HWY_F_HEADING * fstride + idx] = live ? hm_f2bits(v.h) : 0u;
+  st[HWY_F_SPEED * fstride + idx] = live ? hm_f2bits(v.spd) : 0u;
+  st[HWY_F_TSPEED * fstride + idx] = live ? hm_f2bits(v.tsp) : 0u;
+  st[HWY_F_DELTA * fstride + idx] = live ? hm_f2bits(v.dlt) : 0u;
+  st[HWY_F_TIMER * fstride + idx] = live ? hm_f2bits(v.tmr) : 0u;
+  st[HWY_F_IMPX * fstride + idx] = (live && v.imp) ? hm_f2bits(v.ix) : 0u;
+  st[HWY_F_IMPY * fstride + idx] = (live && v.imp) ? hm_f2bits(v.iy) : 0u;
+  st[HWY_F_LANE * fstride + idx] = live ? (uint32_t)v.ln : 0u;
+  st[HWY_F_TLANE * fstride + idx] = live ? (uint32_t)v.tl : 0u;
+  st[HWY_F_FLAGS * fstride + idx] =
+      live ? ((v.crashed ? HWY_FLAG_CRASHED : 0u) | (v.imp ? HWY_FLAG_IMPACT : 0u) |
+              (v.present ? HWY_FLAG_PRESENT : 0u))
+           : 0u;
+}
+
+__device__ __forceinline__ void store_env_words(uint32_t* st, size_t fstride, size_t idx, int lane,
+                                                int step, int episode, uint64_t seed, float ego_acc,
+                                                float ego_steer, float ep_return) {
+  uint32_t w = 0u;
+  if (lane == HWY_E_STEP) w = (uint32_t)step;
+  if (lane == HWY_E_EPISODE) w = (uint32_t)episode;
+  if (lane == HWY_E_SEED_LO) w = (uint32_t)(seed & 0xffffffffu);
+  if (lane == HWY_E_SEED_HI) w = (uint32_t)(seed >> 32);
+  if (lane == HWY_E_EGO_ACC) w = hm_f2bits(ego_acc);
+  if (lane == HWY_E_EGO_STEER) w = hm_f2bits(ego_steer);
+  if (lane == HWY_E_RETURN) w = hm_f2bits(ep_return);
+  st[HWY_F_ENV * fstride + idx] = w;
+}
+
+// ------------------------------------------------------------------------- one frame
+// Road.act() then Road.step(dt) for the env of this wave (lane = vehicle).
+__device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt) {
+  const int V = C.vehicles_count + 1;
+  const int lanes = C.lanes_count;
+  const float limit = C.speed_limit;
+  const float ch = hm_cosf(v.h), sh = hm_sinf(v.h);
+  const uint64_t pres = ballot(v.present);
+
+  // ---------------- Road.act: IDMVehicle.act for every non-crashed traffic car
+  const bool actor = v.present && lane >= 1 && !v.crashed;
+  const int tl_old = v.tl;
+  const bool mid = v.ln != v.tl;
+  const bool fire = actor && !mid && (LANE_CHANGE_DELAY < v.tmr);  // utils.do_every
+  if (fire) v.tmr = 0.0f;
+
+  // Road.neighbour_vehicles on lanes ln-1, ln, ln+1 in one pass (slot s <-> lane ln-1+s)
+  int fi[3] = {-1, -1, -1}, ri[3] = {-1, -1, -1};
+  float fsv[3] = {0.0f, 0.0f, 0.0f}, rsv[3] = {0.0f, 0.0f, 0.0f};
+  for (int k = 0; k < V; ++k) {
+    if (!((pres >> k) & 1ull)) continue;
+    const float xk = rdlf(v.x, k), yk = rdlf(v.y, k);
+    const bool ok = (k != lane) && (-LANE_VEH_LEN <= xk) && (xk < ROAD_LENGTH + LANE_VEH_LEN);
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const bool on = ok && hm_absf(lane_lat(yk, v.ln - 1 + s)) <= LANE_WIDTH / 2.0f + 1.0f;
+      if (on && v.x <= xk && (fi[s] < 0 || xk <= fsv[s])) {
+        fsv[s] = xk;
+        fi[s] = k;
+      }
+      if (on && xk < v.x && (ri[s] < 0 || xk > rsv[s])) {
+        rsv[s] = xk;
+        ri[s] = k;
+      }
+    }
+  }
+
+  // gathers (all lanes active)
+  const int sop = fi[1] >= 0 ? fi[1] : lane;
+  const float op_x = shf(v.x, sop), op_spd = shf(v.spd, sop), op_c = shf(ch, sop),
+              op_s = shf(sh, sop);
+  float np_x[2], np_spd[2], np_c[2], np_s[2], nf_x[2], nf_spd[2], nf_c[2], nf_s[2], nf_tsp[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int s = 2 * q;  // slot 0 (left, ln-1) and slot 2 (right, ln+1)
+    const int a = fi[s] >= 0 ? fi[s] : lane;
+    const int b = ri[s] >= 0 ? ri[s] : lane;
+    np_x[q] = shf(v.x, a);
+    np_spd[q] = shf(v.spd, a);
+    np_c[q] = shf(ch, a);
+    np_s[q] = shf(sh, a);
+    nf_x[q] = shf(v.x, b);
+    nf_spd[q] = shf(v.spd, b);
+    nf_c[q] = shf(ch, b);
+    nf_s[q] = shf(sh, b);
+    const float tsp_b = shf(v.tsp, b);  // unconditional: ds_bpermute needs all lanes active
+    nf_tsp[q] = (b == 0) ? 0.0f : tsp_b;  // plain Vehicle (ego) has no target_speed
+  }
+
+  // acceleration(self, front on own lane): IDM term and MOBIL's self_a
+  float self_a = 0.0f;
+  if (actor)
+    self_a = idm_acc(v.spd, v.tsp, v.x, ch, sh, fi[1] >= 0, op_x, op_spd, op_c, op_s, v.dlt, limit);
+
+  // IDMVehicle.change_lane_policy -> mobil, side lanes left then right (POLITENESS = 0, so the
+  // followers' unchanged-lane terms multiply by zero and are not evaluated)
+  int ntl = v.tl;
+  if (fire) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c = v.ln - 1 + 2 * q;
+      const int s = 2 * q;
+      if (c < 0 || c >= lanes) continue;
+      if (!(hm_absf(lane_lat(v.y, c)) <= 2.0f * LANE_WIDTH && 0.0f <= v.x &&
+            v.x < ROAD_LENGTH + LANE_VEH_LEN))
+        continue;  // is_reachable_from
+      if (hm_absf(v.spd) < 1.0f) continue;
+      float nfp = 0.0f;
+      if (ri[s] >= 0)
+        nfp = idm_acc(nf_spd[q], nf_tsp[q], nf_x[q], nf_c[q], nf_s[q], true, v.x, v.spd, ch, sh,
+                      v.dlt, limit);
+      if (nfp < -LANE_CHANGE_MAX_BRAKING_IMPOSED) continue;
+      const float spa = idm_acc(v.spd, v.tsp, v.x, ch, sh, fi[s] >= 0, np_x[q], np_spd[q], np_c[q],
+                                np_s[q], v.dlt, limit);
+      if ((spa - self_a) < LANE_CHANGE_MIN_ACC_GAIN) continue;
+      ntl = c;
+    }
+  }
+
+  // abort an ongoing lane change if another car targets the same lane within its desired gap,
+  // in road order (lower indices already final, higher ones at their frame-start target)
+  int tl_cur = ntl;
+  uint64_t cm = ballot(actor && mid);
+  while (cm) {
+    const int j = __builtin_ctzll(cm);
+    cm &= cm - 1ull;
+    const int tj = rdli(tl_cur, j);
+    const float xj = rdlf(v.x, j), vj = rdlf(v.spd, j), cj = rdlf(ch, j), sj = rdlf(sh, j);
+    const int vis = (lane < j) ? tl_cur : tl_old;
+    const float d = v.x - xj;
+    const float d_star = desired_gap(vj, cj, sj, v.spd, ch, sh);
+    const bool cond = v.present && lane != j && lane != 0 && v.ln != tj && vis == tj &&
+                      (0.0f < d) && (d < d_star);
+    if (wave_any(cond) && lane == j) tl_cur = v.ln;
+  }
+  v.tl = tl_cur;
+
+  // IDM on the target lane while changing lanes
+  const bool need_t = actor && v.ln != v.tl;
+  int ft = -1;
+  if (v.tl == v.ln - 1) ft = fi[0];
+  if (v.tl == v.ln + 1) ft = fi[2];
+  const bool extra = need_t && !(v.tl == v.ln - 1 || v.tl == v.ln + 1);
+  if (wave_any(extra)) {  // target lane not adjacent (rare): dedicated scan
+    float fsx = 0.0f;
+    int fx = -1;
+    for (int k = 0; k < V; ++k) {
+      if (!((pres >> k) & 1ull)) continue;
+      const float xk = rdlf(v.x, k), yk = rdlf(v.y, k);
+      const bool on = (k != lane) && (-LANE_VEH_LEN <= xk) && (xk < ROAD_LENGTH + LANE_VEH_LEN) &&
+                      hm_absf(lane_lat(yk, v.tl)) <= LANE_WIDTH / 2.0f + 1.0f;
+      if (on && v.x <= xk && (fx < 0 || xk <= fsx)) {
+        fsx = xk;
+        fx = k;
+      }
+    }
+    if (extra) ft = fx;
+  }
+  const int st_ = ft >= 0 ? ft : lane;
+  const float ft_x = shf(v.x, st_), ft_spd = shf(v.spd, st_), ft_c = shf(ch, st_),
+              ft_s = shf(sh, st_);
+  if (actor) {
+    float steer = steering_control(v.y, v.h, v.spd, v.tl);
+    steer = hm_clipf(steer, -MAX_STEERING, MAX_STEERING);
+    float acc = self_a;
+    if (need_t) {
+      const float acc_t =
+          idm_acc(v.spd, v.tsp, v.x, ch, sh, ft >= 0, ft_x, ft_spd, ft_c, ft_s, v.dlt, limit);
+      acc = hm_minf(acc, acc_t);
+    }
+    acc = hm_clipf(acc, -ACC_MAX, ACC_MAX);
+    v.asteer = steer;
+    v.aacc = acc;
+  }
+
+  // ---------------- Road.step: Vehicle.step for every vehicle
+  if (v.present) {
+    if (lane != 0) v.tmr = v.tmr + dt;  // IDMVehicle.step
+    if (v.crashed) {                    // clip_actions
+      v.asteer = 0.0f;
+      v.aacc = -1.0f * v.spd;
+    }
+    if (v.spd > MAX_SPEED) {
+      v.aacc = hm_minf(v.aacc, 1.0f * (MAX_SPEED - v.spd));
+    } else if (v.spd < MIN_SPEED) {
+      v.aacc = hm_maxf(v.aacc, 1.0f * (MIN_SPEED - v.spd));
+    }
+    const float beta = hm_atanf(0.5f * hm_tanf(v.asteer));
+    const float vx = v.spd * hm_cosf(v.h + beta);
+    const float vy = v.spd * hm_sinf(v.h + beta);
+    v.x = v.x + vx * dt;
+    v.y = v.y + vy * dt;
+    if (v.imp) {
+      v.x = v.x + v.ix;
+      v.y = v.y + v.iy;
+      v.crashed = true;
+      v.imp = false;
+    }
+    v.h = v.h + v.spd * hm_sinf(beta) / (VEH_LENGTH / 2.0f) * dt;
+    v.spd = v.spd + v.aacc * dt;
+    v.ln = closest_lane(v.y, lanes);  // on_state_update
+  }
+
+  // ---------------- Road.step: handle_collisions for every pair, a = lower index
+  const float c2 = hm_cosf(v.h), s2 = hm_sinf(v.h);
+  const float dax_self = (v.spd * c2) * dt, day_self = (v.spd * s2) * dt;
+  uint64_t pm = 0ull;
+  for (int k = 0; k < V; ++k) {
+    if (!((pres >> k) & 1ull)) continue;
+    const float xk = rdlf(v.x, k), yk = rdlf(v.y, k), vk = rdlf(v.spd, k);
+    const bool lower = lane < k;
+    const float dx = lower ? (xk - v.x) : (v.x - xk);
+    const float dy = lower ? (yk - v.y) : (v.y - yk);
+    const float va = lower ? v.spd : vk;
+    const bool pass = v.present && k != lane &&
+                      !(__builtin_sqrtf(dx * dx + dy * dy) >
+                        (VEH_DIAGONAL + VEH_DIAGONAL) / 2.0f + va * dt);
+    if (pass) pm |= (1ull << k);
+  }
+  while (wave_any(pm != 0ull)) {
+    const bool has = pm != 0ull;
+    const int j = has ? __builtin_ctzll(pm) : lane;
+    if (has) pm &= pm - 1ull;
+    const float xj = shf(v.x, j), yj = shf(v.y, j), cj = shf(c2, j), sj = shf(s2, j),
+                vj = shf(v.spd, j);
+    const float daxj = (vj * cj) * dt, dayj = (vj * sj) * dt;
+    const bool lower = lane < j;
+    bool inter, will;
+    float tx, ty;
+    sat_collide(lower ? v.x : xj, lower ? v.y : yj, lower ? c2 : cj, lower ? s2 : sj,
+                lower ? dax_self : daxj, lower ? day_self : dayj, lower ? xj : v.x,
+                lower ? yj : v.y, lower ? cj : c2, lower ? sj : s2, lower ? daxj : dax_self,
+                lower ? dayj : day_self, &inter, &will, &tx, &ty);
+    if (has) {
+      if (will) {
+        v.ix = lower ? tx / 2.0f : -tx / 2.0f;
+        v.iy = lower ? ty / 2.0f : -ty / 2.0f;
+        v.imp = true;
+      }
+      if (inter) v.crashed = true;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------- kernels
+__global__ void __launch_bounds__(256) hwy_step_kernel(StepParams P) {
+  __shared__ int lds_vor[ENVS_PER_BLOCK][WAVE];
+  __shared__ int lds_inv[ENVS_PER_BLOCK][WAVE];
+  const hwy_config& C = P.cfg;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int w = threadIdx.x / WAVE;
+  const int e = blockIdx.x * ENVS_PER_BLOCK + w;
+  if (e >= C.num_envs) return;  // whole wave
+  const int V = C.vehicles_count + 1;
+  const size_t fstride = (size_t)C.num_envs * WAVE;
+  const size_t idx = (size_t)e * WAVE + lane;
+  uint32_t* st = P.state;
+
+  Veh v;
+  load_veh(st, fstride, idx, lane, V, v);
+  const uint32_t ew = st[HWY_F_ENV * fstride + idx];
+  int step = rdli((int)ew, HWY_E_STEP);
+  int episode = rdli((int)ew, HWY_E_EPISODE);
+  uint64_t seed = (uint64_t)(uint32_t)rdli((int)ew, HWY_E_SEED_LO) |
+                  ((uint64_t)(uint32_t)rdli((int)ew, HWY_E_SEED_HI) << 32);
+  float ep_return = hm_bits2f((uint32_t)rdli((int)ew, HWY_E_RETURN));
+  if (lane == 0) {
+    v.aacc = hm_bits2f((uint32_t)rdli((int)ew, HWY_E_EGO_ACC));
+    v.asteer = hm_bits2f((uint32_t)rdli((int)ew, HWY_E_EGO_STEER));
+  }
+
+  const float dt = 1.0f / (float)C.sim_freq;
+  const int frames = C.sim_freq / C.policy_freq;
+  const float a0 = P.actions[2 * (size_t)e], a1 = P.actions[2 * (size_t)e + 1];
+  for (int frame = 0; frame < frames; ++frame) {
+    if (frame == 0 && lane == 0) {  // ContinuousAction.act
+      v.aacc = hm_lmap(hm_clipf(a0, -1.0f, 1.0f), -1.0f, 1.0f, -5.0f, 5.0f);
+      v.asteer = hm_lmap(hm_clipf(a1, -1.0f, 1.0f), -1.0f, 1.0f, -HM_PIO4_F, HM_PIO4_F);
+    }
+    frame_wave(C, lane, v, dt);
+  }
+  step += 1;
+
+  // HighwayEnv._reward / _is_terminated / _is_truncated on the ego (lane 0)
+  float rew = 0.0f;
+  int terminated = 0;
+  if (lane == 0) {
+    const float forward_speed = v.spd * hm_cosf(v.h);
+    const float scaled_speed = hm_lmap(forward_speed, C.reward_speed_range[0],
+                                       C.reward_speed_range[1], 0.0f, 1.0f);
+    const float collision = v.crashed ? 1.0f : 0.0f;
+    const int nl = C.lanes_count - 1;
+    const float right_lane = (float)v.ln / (float)(nl > 1 ? nl : 1);
+    const float high_speed = hm_clipf(scaled_speed, 0.0f, 1.0f);
+    const bool on_road = on_lane_m(v.x, v.y, v.ln, 0.0f);
+    const float on_road_f = on_road ? 1.0f : 0.0f;
+    rew = 0.0f;
+    rew = rew + C.collision_reward * collision;
+    rew = rew + C.right_lane_reward * right_lane;
+    rew = rew + C.high_speed_reward * high_speed;
+    rew = rew + C.on_road_reward * on_road_f;
+    if (C.normalize_reward)
+      rew = hm_lmap(rew, C.collision_reward, C.high_speed_reward + C.right_lane_reward, 0.0f, 1.0f);
+    rew = rew * on_road_f;
+    terminated = v.crashed || (C.offroad_terminal && !on_road);
+  }
+  rew = rdlf(rew, 0);
+  terminated = rdli(terminated, 0);
+  const int truncated = step >= C.max_steps;
+  ep_return = ep_return + rew;
+  const bool done = terminated || truncated;
+  if (lane == 0) {
+    P.reward[e] = rew;
+    P.term[e] = (uint8_t)terminated;
+    P.trunc[e] = (uint8_t)truncated;
+    if (P.ep_ret) P.ep_ret[e] = done ? ep_return : 0.0f;
+    if (P.ep_len) P.ep_len[e] = done ? step : 0;
+  }
+  if (done && C.autoreset) {
+    episode += 1;
+    seed = schedule_seed(C, e, episode);
+    reset_wave(C, lane, seed, v);
+    step = 0;
+    ep_return = 0.0f;
+  }
+  observe_wave(C, lane, v, step, seed, P.pe_table, P.obs + (size_t)e * C.obs_vehicles * P.fout,
+               P.fout, lds_vor[w], lds_inv[w]);
+  store_veh(st, fstride, idx, lane, V, v);
+  store_env_words(st, fstride, idx, lane, step, episode, seed, rdlf(v.aacc, 0), rdlf(v.asteer, 0),
+                  ep_return);
+}
+
+__global__ void __launch_bounds__(256) hwy_reset_kernel(StepParams P) {
+  __shared__ int lds_vor[ENVS_PER_BLOCK][WAVE];
+  __shared__ int lds_inv[ENVS_PER_BLOCK][WAVE];
+  const hwy_config& C = P.cfg;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int w = threadIdx.x / WAVE;
+  const int e = blockIdx.x * ENVS_PER_BLOCK + w;
+  if (e >= C.num_envs) return;
+  if (P.mask && !P.mask[e]) return;
+  const int V = C.vehicles_count + 1;
+  const size_t fstride = (size_t)C.num_envs * WAVE;
+  const size_t idx = (size_t)e * WAVE + lane;
+  const uint64_t seed = P.seeds ? P.seeds[e] : schedule_seed(C, e, 0);
+  Veh v;
+  reset_wave(C, lane, seed, v);
+  if (P.obs)
+    observe_wave(C, lane, v, 0, seed, P.pe_table, P.obs + (size_t)e * C.obs_vehicles * P.fout,
+                 P.fout, lds_vor[w], lds_inv[w]);
+  store_veh(P.state, fstride, idx, lane, V, v);
+  store_env_words(P.state, fstride, idx, lane, 0, 0, seed, 0.0f, 0.0f, 0.0f);
+}
+
+// Stand-alone wrapper on [E,N,F]: one thread per (env, row).
+__global__ void __launch_bounds__(256) hwy_obs_pe_kernel(const float* __restrict__ in,
+                                                         float* __restrict__ out, int E, int N,
+                                                         int F, int kind, int d, int ego_idx,
+                                                         float max_dist, const float* table,
+                                                         const float* dist_override) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)E * N) return;
+  const long e = t / N;
+  const int r = (int)(t - e * N);
+  const int Fo = F + ((kind == HWY_PE_RANK || kind == HWY_PE_DIST) ? d : 0);
+  float vals[HWY_MAX_FEATURES];
+#pragma unroll
+  for (int f = 0; f < HWY_MAX_FEATURES; ++f) vals[f] = f < F ? in[t * F + f] : 0.0f;
+  const float* eg = in + (e * N + ego_idx) * F;
+  const float ex0 = eg[0], ex1 = F > 1 ? eg[1] : 0.0f;
+  write_pe_row(vals, F, kind, d, r, ex0, ex1, max_dist, table, dist_override != nullptr,
+               dist_override ? dist_override[t] : 0.0f, out + t * Fo);
+}
+
+// PPOMemory.compute_advantages on [T,E]: one thread per env, reversed scan over t.
+__global__ void __launch_bounds__(256) hwy_gae_kernel(const float* __restrict__ rew,
+                                                      const uint8_t* __restrict__ done,
+                                                      const float* __restrict__ val,
+                                                      const float* __restrict__ last_val,
+                                                      double gamma, double lam, int T, int E,
+                                                      float* __restrict__ adv,
+                                                      float* __restrict__ ret) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const double gl = gamma * lam;
+  float last_adv = 0.0f;
+  double v1 = (double)last_val[e];
+  for (int t = T - 1; t >= 0; --t) {
+    const size_t i = (size_t)t * E + e;
+    const float v0f = val[i];
+    const double nd = done[i] ? 0.0 : 1.0;
+    const double delta = ((double)rew[i] + (gamma * v1) * nd) - (double)v0f;
+    const float a = (float)(delta + (gl * nd) * (double)last_adv);
+    adv[i] = a;
+    ret[i] = a + v0f;
+    last_adv = a;
+    v1 = (double)v0f;
+  }
+}
+
+__global__ void hwy_math_kernel(int op, const float* in, const float* in2, float* out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float x = in[i], y = in2 ? in2[i] : 0.0f;
+  float r = 0.0f;
+  switch (op) {
+    case 0: r = hm_sinf(x); break;
+    case 1: r = hm_cosf(x); break;
+    case 2: r = hm_tanf(x); break;
+    case 3: r = hm_atanf(x); break;
+    case 4: r = hm_asinf(x); break;
+    case 5: r = hm_expf(x); break;
+    case 6: r = hm_logf(x); break;
+    case 7: r = hm_powf(x, y); break;
+    case 8: r = hm_wrap_to_pi(x); break;
+    case 9: r = __builtin_sqrtf(x); break;
+    case 10: r = x / y; break;
+    case 11: r = hm_floorf(x); break;
+  }
+  out[i] = r;
+}
+
+// ------------------------------------------------------------------------- launch helpers
+extern "C" {
+int hwy_launch_step(const StepParams* p, hipStream_t s) {
+  const int blocks = (p->cfg.num_envs + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
+  hipLaunchKernelGGL(hwy_step_kernel, dim3(blocks), dim3(ENVS_PER_BLOCK * WAVE), 0, s, *p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int hwy_launch_reset(const StepParams* p, hipStream_t s) {
+  const int blocks = (p->cfg.num_envs + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
+  hipLaunchKernelGGL(hwy_reset_kernel, dim3(blocks), dim3(ENVS_PER_BLOCK * WAVE), 0, s, *p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int hwy_launch_obs_pe(const float* in, float* out, int E, int N, int F, int kind, int d, int ego,
+                      float max_dist, const float* table, const float* dov, hipStream_t s) {
+  const long n = (long)E * N;
+  if (n == 0) return 0;
+  const int blocks = (int)((n + 255) / 256);
+  hipLaunchKernelGGL(hwy_obs_pe_kernel, dim3(blocks), dim3(256), 0, s, in, out, E, N, F, kind, d,
+                     ego, max_dist, table, dov);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int hwy_launch_gae(const float* rew, const uint8_t* done, const float* val, const float* last_val,
+                   double gamma, double lam, int T, int E, float* adv, float* ret, hipStream_t s) {
+  if (E == 0) return 0;
+  const int blocks = (E + 255) / 256;
+  hipLaunchKernelGGL(hwy_gae_kernel, dim3(blocks), dim3(256), 0, s, rew, done, val, last_val,
+                     gamma, lam, T, E, adv, ret);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int hwy_launch_math(int op, const float* in, const float* in2, float* out, int n, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(hwy_math_kernel, dim3((n + 255) / 256), dim3(256), 0, s, op, in, in2, out, n);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+}

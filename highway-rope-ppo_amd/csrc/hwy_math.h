@@ -1,0 +1,326 @@
+/*
+ * hwy_math.h -- deterministic binary32 math shared by the gfx950 kernels and the host.
+ *
+ * Why: the highway step is chaotic (MOBIL thresholds, collision tests), so GPU/CPU parity is
+ * only meaningful if both sides round identically. libm (glibc) and the device library (ocml)
+ * differ in the last ulp of sin/atan/pow, so both sides use these routines instead. They use
+ * only IEEE-754 correctly rounded operations (+ - * / sqrt, floor, int<->float), so with
+ * -ffp-contract=off they produce the same bits on x86-64 (SSE) and on gfx950.
+ * Polynomials are the classic Cephes single-precision ones (S. Moshier, public domain),
+ * accurate to ~1-3 ulp on the ranges used; tests/test_math.py checks them against libm double.
+ *
+ * Usable from C (gcc) and HIP C++ (hipcc): HWY_HD expands to __host__ __device__ under HIP.
+ */
+#ifndef HWY_MATH_H_
+#define HWY_MATH_H_
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define HWY_HD __host__ __device__ static inline
+#else
+#define HWY_HD static inline
+#endif
+
+#define HM_PI_F 3.14159265358979323846f
+#define HM_PIO2_F 1.5707963267948966192f
+#define HM_PIO4_F 0.7853981633974483096f
+#define HM_TWO_PI_F 6.28318530717958647692f
+
+HWY_HD float hm_bits2f(uint32_t u) {
+  union { uint32_t u; float f; } c;
+  c.u = u;
+  return c.f;
+}
+HWY_HD uint32_t hm_f2bits(float f) {
+  union { uint32_t u; float f; } c;
+  c.f = f;
+  return c.u;
+}
+
+HWY_HD float hm_absf(float x) { return hm_bits2f(hm_f2bits(x) & 0x7fffffffu); }
+HWY_HD int hm_isnan(float x) { return x != x; }
+
+/* numpy.clip semantics for scalars: NaN propagates. */
+HWY_HD float hm_clipf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+HWY_HD float hm_minf(float a, float b) { return (b < a) ? b : a; } /* min(a,b) python */
+HWY_HD float hm_maxf(float a, float b) { return (b > a) ? b : a; } /* max(a,b) python */
+
+/* floor for |x| < 2^31 without libm (exact) */
+HWY_HD float hm_floorf(float x) {
+  if (!(hm_absf(x) < 8388608.0f)) return x; /* already integral, inf or nan */
+  float t = (float)(int32_t)x;              /* truncation, exact */
+  return (t > x) ? t - 1.0f : t;
+}
+
+/* x * 2^n, n in [-300, 300] */
+HWY_HD float hm_ldexpf(float x, int n) {
+  if (n > 127) {
+    x *= hm_bits2f(0x7f000000u); /* 2^127 */
+    n -= 127;
+    if (n > 127) n = 127;
+  }
+  if (n < -126) {
+    x *= hm_bits2f(0x00800000u); /* 2^-126 */
+    n += 126;
+    if (n < -126) {
+      x *= hm_bits2f(0x00800000u);
+      n += 126;
+      if (n < -126) n = -126;
+    }
+  }
+  return x * hm_bits2f((uint32_t)(n + 127) << 23);
+}
+
+/* x = m * 2^e with m in [0.5, 1); x finite > 0 */
+HWY_HD float hm_frexpf(float x, int* e) {
+  uint32_t u = hm_f2bits(x);
+  int ex = (int)((u >> 23) & 0xffu);
+  int adj = 0;
+  if (ex == 0) { /* subnormal: scale by 2^25 */
+    x *= 33554432.0f;
+    u = hm_f2bits(x);
+    ex = (int)((u >> 23) & 0xffu);
+    adj = -25;
+  }
+  *e = ex - 126 + adj;
+  return hm_bits2f((u & 0x807fffffu) | 0x3f000000u);
+}
+
+/* Cephes sinf/cosf core: returns sin (want_cos = 0) or cos (want_cos = 1). */
+HWY_HD float hm_sincos_core(float xx, int want_cos) {
+  const float FOPI = 1.27323954473516f;
+  const float DP1 = 0.78515625f;
+  const float DP2 = 2.4187564849853515625e-4f;
+  const float DP3 = 3.77489497744594108e-8f;
+  float x = xx;
+  int sign = 1;
+  if (x < 0.0f) {
+    x = -x;
+    if (!want_cos) sign = -1;
+  }
+  if (!(x <= 16777215.0f)) return hm_isnan(x) ? x : 0.0f; /* total loss of precision */
+  uint32_t j = (uint32_t)(FOPI * x);
+  float y = (float)j;
+  if (j & 1u) {
+    j += 1u;
+    y += 1.0f;
+  }
+  j &= 7u;
+  if (j > 3u) {
+    sign = -sign;
+    j -= 4u;
+  }
+  if (want_cos && j > 1u) sign = -sign;
+  x = ((x - y * DP1) - y * DP2) - y * DP3;
+  float z = x * x;
+  int use_cos_poly = want_cos ? !(j == 1u || j == 2u) : (j == 1u || j == 2u);
+  float r;
+  if (use_cos_poly) {
+    r = 2.443315711809948E-005f;
+    r = r * z - 1.388731625493765E-003f;
+    r = r * z + 4.166664568298827E-002f;
+    r = r * (z * z);
+    r = r - 0.5f * z;
+    r = r + 1.0f;
+  } else {
+    r = -1.9515295891E-4f;
+    r = r * z + 8.3321608736E-3f;
+    r = r * z - 1.6666654611E-1f;
+    r = r * (z * x);
+    r = r + x;
+  }
+  return sign < 0 ? -r : r;
+}
+HWY_HD float hm_sinf(float x) { return hm_sincos_core(x, 0); }
+HWY_HD float hm_cosf(float x) { return hm_sincos_core(x, 1); }
+HWY_HD float hm_tanf(float x) { return hm_sinf(x) / hm_cosf(x); }
+
+/* Cephes atanf */
+HWY_HD float hm_atanf(float xx) {
+  float x = xx, y;
+  int sign = 1;
+  if (xx < 0.0f) {
+    sign = -1;
+    x = -xx;
+  }
+  if (x > 2.414213562373095f) {
+    y = HM_PIO2_F;
+    x = -(1.0f / x);
+  } else if (x > 0.4142135623730950f) {
+    y = HM_PIO4_F;
+    x = (x - 1.0f) / (x + 1.0f);
+  } else {
+    y = 0.0f;
+  }
+  float z = x * x;
+  float p = 8.05374449538e-2f;
+  p = p * z - 1.38776856032E-1f;
+  p = p * z + 1.99777106478E-1f;
+  p = p * z - 3.33329491539E-1f;
+  y = y + (p * z * x + x);
+  return sign < 0 ? -y : y;
+}
+
+/* Cephes asinf; caller clips to [-1, 1] (np.arcsin(np.clip(...)) in the reference). */
+HWY_HD float hm_asinf(float xx) {
+  float a, x = xx, z;
+  int sign, flag;
+  if (x > 0.0f) {
+    sign = 1;
+    a = x;
+  } else {
+    sign = -1;
+    a = -x;
+  }
+  if (a > 1.0f) return 0.0f / 0.0f;
+  if (a < 1.0e-4f) {
+    z = a;
+  } else {
+    if (a > 0.5f) {
+      z = 0.5f * (1.0f - a);
+      x = __builtin_sqrtf(z);
+      flag = 1;
+    } else {
+      x = a;
+      z = x * x;
+      flag = 0;
+    }
+    float p = 4.2163199048E-2f;
+    p = p * z + 2.4181311049E-2f;
+    p = p * z + 4.5470025998E-2f;
+    p = p * z + 7.4953002686E-2f;
+    p = p * z + 1.6666752422E-1f;
+    z = p * z * x + x;
+    if (flag) {
+      z = z + z;
+      z = HM_PIO2_F - z;
+    }
+  }
+  return sign < 0 ? -z : z;
+}
+
+/* Cephes expf */
+HWY_HD float hm_expf(float xx) {
+  float x = xx;
+  if (hm_isnan(x)) return x;
+  if (x > 88.72283905206835f) return hm_bits2f(0x7f800000u);
+  if (x < -103.278929903431851103f) return 0.0f;
+  float z = hm_floorf(1.44269504088896341f * x + 0.5f);
+  x = x - z * 0.693359375f;
+  x = x - z * -2.12194440e-4f;
+  int n = (int)z;
+  z = x * x;
+  float p = 1.9875691500E-4f;
+  p = p * x + 1.3981999507E-3f;
+  p = p * x + 8.3334519073E-3f;
+  p = p * x + 4.1665795894E-2f;
+  p = p * x + 1.6666665459E-1f;
+  p = p * x + 5.0000001201E-1f;
+  p = p * z + x + 1.0f;
+  return hm_ldexpf(p, n);
+}
+
+/* Cephes logf (x > 0 finite; 0 -> -inf; <0 -> nan) */
+HWY_HD float hm_logf(float xx) {
+  float x = xx;
+  if (hm_isnan(x)) return x;
+  if (x <= 0.0f) return x == 0.0f ? hm_bits2f(0xff800000u) : 0.0f / 0.0f;
+  if (x == hm_bits2f(0x7f800000u)) return x;
+  int e;
+  x = hm_frexpf(x, &e);
+  if (x < 0.707106781186547524f) {
+    e -= 1;
+    x = (x + x) - 1.0f;
+  } else {
+    x = x - 1.0f;
+  }
+  float z = x * x;
+  float y = 7.0376836292E-2f;
+  y = y * x - 1.1514610310E-1f;
+  y = y * x + 1.1676998740E-1f;
+  y = y * x - 1.2420140846E-1f;
+  y = y * x + 1.4249322787E-1f;
+  y = y * x - 1.6668057665E-1f;
+  y = y * x + 2.0000714765E-1f;
+  y = y * x - 2.4999993993E-1f;
+  y = y * x + 3.3333331174E-1f;
+  y = y * x * z;
+  float fe = (float)e;
+  if (e) y = y + -2.12194440e-4f * fe;
+  y = y + -0.5f * z;
+  z = x + y;
+  if (e) z = z + 0.693359375f * fe;
+  return z;
+}
+
+/* np.power(b, p) for b >= 0 (IDM: max(v,0)/|v0| ** DELTA) */
+HWY_HD float hm_powf(float b, float p) {
+  if (b == 0.0f) return p > 0.0f ? 0.0f : (p == 0.0f ? 1.0f : hm_bits2f(0x7f800000u));
+  if (b == 1.0f || p == 0.0f) return 1.0f;
+  return hm_expf(p * hm_logf(b));
+}
+
+/* utils.wrap_to_pi: ((x + pi) % (2 pi)) - pi with Python's floored modulo. */
+HWY_HD float hm_wrap_to_pi(float x) {
+  float t = x + HM_PI_F;
+  float n = hm_floorf(t / HM_TWO_PI_F);
+  float r = t - n * HM_TWO_PI_F;
+  if (r < 0.0f) r = r + HM_TWO_PI_F;
+  if (r >= HM_TWO_PI_F) r = r - HM_TWO_PI_F;
+  return r - HM_PI_F;
+}
+
+/* utils.not_zero(x, eps=1e-2) */
+HWY_HD float hm_not_zero(float x) {
+  if (hm_absf(x) > 1e-2f) return x;
+  return x >= 0.0f ? 1e-2f : -1e-2f;
+}
+
+/* utils.lmap(v, [x0, x1], [y0, y1]) = y0 + (v - x0) * (y1 - y0) / (x1 - x0) */
+HWY_HD float hm_lmap(float v, float x0, float x1, float y0, float y1) {
+  return y0 + (v - x0) * (y1 - y0) / (x1 - x0);
+}
+
+/* ---------------------------------------------------------------------------------------
+ * Philox4x32-10 (Salmon et al., SC'11), counter-based RNG for traffic generation and the
+ * "shuffled" row permutation. Verified against the Random123 known-answer vectors.
+ * ------------------------------------------------------------------------------------- */
+typedef struct hm_u32x4 {
+  uint32_t v[4];
+} hm_u32x4;
+
+HWY_HD hm_u32x4 hm_philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                 uint32_t k1) {
+  for (int r = 0; r < 10; ++r) {
+    if (r > 0) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)c0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c2;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c1 ^ k0;
+    uint32_t n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+  }
+  hm_u32x4 o;
+  o.v[0] = c0;
+  o.v[1] = c1;
+  o.v[2] = c2;
+  o.v[3] = c3;
+  return o;
+}
+
+/* uniform [0, 1) with 24 random bits (exact in binary32) */
+HWY_HD float hm_u01(uint32_t u) { return (float)(u >> 8) * 5.9604644775390625e-8f; }
+/* np_random.uniform(lo, hi) */
+HWY_HD float hm_uniform(uint32_t u, float lo, float hi) { return lo + (hi - lo) * hm_u01(u); }
+/* np_random.choice(n): multiply-shift bounded integer */
+HWY_HD int hm_choice(uint32_t u, int n) { return (int)(((uint64_t)u * (uint64_t)n) >> 32); }
+
+#endif /* HWY_MATH_H_ */

@@ -1,0 +1,813 @@
+/*
+ * oracle/hwy_oracle.c -- CPU restatement of the reference hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library,
+ * and only as the checker / the timed CPU baseline.  The product path (libhwy.so, HIP) never
+ * links or calls it.
+ *
+ * What it restates (reference = DhruvDh/highway-rope-ppo; "upstream" = highway-env 1.10.1, the
+ * third-party package the reference drives through gym.make("highway-v0") at
+ * experiments/wrappers.py:80, pinned at uv.lock:163-178, not vendored and not installed here):
+ *   - the highway-v0 step, reset and Kinematics observation, written scalar and sequential in
+ *     upstream's object order (Road.act -> IDMVehicle.act for each vehicle in list order,
+ *     Road.step -> Vehicle.step, pairwise handle_collisions for i < j).  Upstream's source is not
+ *     available offline: these functions follow its published algorithm and are PARITY UNPINNED
+ *     against upstream (see DESIGN.md "Oracle").  Deviations by design: binary32 arithmetic,
+ *     Philox traffic RNG instead of numpy PCG64, configurable horizon.
+ *   - the observation wrappers: experiments/rope_embed.py:44-74, dist_embed.py:76-96,
+ *     rank_embed.py:45-51 (pinned by tests/golden fixtures generated from the reference);
+ *   - GAE: ppo/agent.py:126-138 (pinned by tests/golden fixtures generated from the reference).
+ *
+ * State layout and config are those of include/hwy.h, so the oracle and libhwy.so can exchange
+ * states and be compared bit for bit.  Both use the deterministic math of hwy_math.h.
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/hwy.h"
+#include "../highway-rope-ppo_amd/csrc/hwy_math.h"
+
+/* ---- upstream constants (highway_env vehicle/, road/lane.py, envs/common/abstract.py) ---- */
+#define LANE_WIDTH 4.0f          /* AbstractLane.DEFAULT_WIDTH */
+#define LANE_VEH_LEN 5.0f        /* AbstractLane.VEHICLE_LENGTH */
+#define ROAD_LENGTH 10000.0f     /* straight_road_network length */
+#define VEH_LENGTH 5.0f          /* Vehicle.LENGTH */
+#define VEH_WIDTH 2.0f           /* Vehicle.WIDTH */
+#define MAX_SPEED 40.0f          /* Vehicle.MAX_SPEED */
+#define MIN_SPEED (-40.0f)
+#define KP_A (1.0f / 0.6f)       /* ControlledVehicle 1/TAU_ACC (unused by IDM) */
+#define KP_HEADING (1.0f / 0.2f) /* 1/TAU_HEADING */
+#define KP_LATERAL (1.0f / 0.6f) /* 1/TAU_LATERAL */
+#define MAX_STEERING (HM_PI_F / 3.0f)
+#define ACC_MAX 6.0f             /* IDMVehicle.ACC_MAX */
+#define COMFORT_ACC_MAX 3.0f
+#define COMFORT_ACC_MIN (-5.0f)
+#define DISTANCE_WANTED 10.0f    /* 5.0 + ControlledVehicle.LENGTH */
+#define TIME_WANTED 1.5f
+#define POLITENESS 0.0f
+#define LANE_CHANGE_MIN_ACC_GAIN 0.2f
+#define LANE_CHANGE_MAX_BRAKING_IMPOSED 2.0f
+#define LANE_CHANGE_DELAY 1.0f
+#define PERCEPTION_DISTANCE 200.0f /* 5 * Vehicle.MAX_SPEED */
+#define TWO_SQRT_AB 7.745966692414834f /* 2 * sqrt(-COMFORT_ACC_MAX * COMFORT_ACC_MIN) */
+#define VEH_DIAGONAL 5.385164807134504f /* sqrt(LENGTH^2 + WIDTH^2) */
+
+typedef struct {
+  float x, y, heading, speed;
+  float target_speed, delta, timer;
+  float imp_x, imp_y;
+  int has_impact;
+  int lane, target_lane;
+  int crashed, present;
+  float act_steer, act_acc; /* Vehicle.action dict */
+} Veh;
+
+typedef struct {
+  const hwy_config* cfg;
+  int V;
+  Veh v[HWY_MAX_VEHICLES];
+  int step, episode;
+  uint64_t seed;
+  float ep_return;
+  float dt;
+} Road;
+
+/* ------------------------------------------------------------------ state packing */
+static inline uint32_t* fld(uint32_t* st, int f, int E, int e) {
+  return st + ((size_t)f * (size_t)E + (size_t)e) * HWY_MAX_VEHICLES;
+}
+
+static void load_road(Road* r, const hwy_config* cfg, uint32_t* st, int E, int e) {
+  r->cfg = cfg;
+  r->V = cfg->vehicles_count + 1;
+  r->dt = 1.0f / (float)cfg->sim_freq;
+  for (int i = 0; i < r->V; ++i) {
+    Veh* v = &r->v[i];
+    v->x = hm_bits2f(fld(st, HWY_F_X, E, e)[i]);
+    v->y = hm_bits2f(fld(st, HWY_F_Y, E, e)[i]);
+    v->heading = hm_bits2f(fld(st, HWY_F_HEADING, E, e)[i]);
+    v->speed = hm_bits2f(fld(st, HWY_F_SPEED, E, e)[i]);
+    v->target_speed = hm_bits2f(fld(st, HWY_F_TSPEED, E, e)[i]);
+    v->delta = hm_bits2f(fld(st, HWY_F_DELTA, E, e)[i]);
+    v->timer = hm_bits2f(fld(st, HWY_F_TIMER, E, e)[i]);
+    v->imp_x = hm_bits2f(fld(st, HWY_F_IMPX, E, e)[i]);
+    v->imp_y = hm_bits2f(fld(st, HWY_F_IMPY, E, e)[i]);
+    v->lane = (int)fld(st, HWY_F_LANE, E, e)[i];
+    v->target_lane = (int)fld(st, HWY_F_TLANE, E, e)[i];
+    uint32_t fl = fld(st, HWY_F_FLAGS, E, e)[i];
+    v->crashed = (fl & HWY_FLAG_CRASHED) != 0;
+    v->has_impact = (fl & HWY_FLAG_IMPACT) != 0;
+    v->present = (fl & HWY_FLAG_PRESENT) != 0;
+    v->act_steer = 0.0f;
+    v->act_acc = 0.0f;
+  }
+  uint32_t* ew = fld(st, HWY_F_ENV, E, e);
+  r->step = (int)ew[HWY_E_STEP];
+  r->episode = (int)ew[HWY_E_EPISODE];
+  r->seed = (uint64_t)ew[HWY_E_SEED_LO] | ((uint64_t)ew[HWY_E_SEED_HI] << 32);
+  r->v[0].act_acc = hm_bits2f(ew[HWY_E_EGO_ACC]);
+  r->v[0].act_steer = hm_bits2f(ew[HWY_E_EGO_STEER]);
+  r->ep_return = hm_bits2f(ew[HWY_E_RETURN]);
+}
+
+static void store_road(const Road* r, uint32_t* st, int E, int e) {
+  for (int i = 0; i < HWY_MAX_VEHICLES; ++i) {
+    if (i >= r->V) {
+      for (int f = 0; f < HWY_F_ENV; ++f) fld(st, f, E, e)[i] = 0u;
+      continue;
+    }
+    const Veh* v = &r->v[i];
+    fld(st, HWY_F_X, E, e)[i] = hm_f2bits(v->x);
+    fld(st, HWY_F_Y, E, e)[i] = hm_f2bits(v->y);
+    fld(st, HWY_F_HEADING, E, e)[i] = hm_f2bits(v->heading);
+    fld(st, HWY_F_SPEED, E, e)[i] = hm_f2bits(v->speed);
+    fld(st, HWY_F_TSPEED, E, e)[i] = hm_f2bits(v->target_speed);
+    fld(st, HWY_F_DELTA, E, e)[i] = hm_f2bits(v->delta);
+    fld(st, HWY_F_TIMER, E, e)[i] = hm_f2bits(v->timer);
+    fld(st, HWY_F_IMPX, E, e)[i] = hm_f2bits(v->has_impact ? v->imp_x : 0.0f);
+    fld(st, HWY_F_IMPY, E, e)[i] = hm_f2bits(v->has_impact ? v->imp_y : 0.0f);
+    fld(st, HWY_F_LANE, E, e)[i] = (uint32_t)v->lane;
+    fld(st, HWY_F_TLANE, E, e)[i] = (uint32_t)v->target_lane;
+    fld(st, HWY_F_FLAGS, E, e)[i] = (v->crashed ? HWY_FLAG_CRASHED : 0u) |
+                                    (v->has_impact ? HWY_FLAG_IMPACT : 0u) |
+                                    (v->present ? HWY_FLAG_PRESENT : 0u);
+  }
+  uint32_t* ew = fld(st, HWY_F_ENV, E, e);
+  for (int w = 0; w < HWY_MAX_VEHICLES; ++w) ew[w] = 0u;
+  ew[HWY_E_STEP] = (uint32_t)r->step;
+  ew[HWY_E_EPISODE] = (uint32_t)r->episode;
+  ew[HWY_E_SEED_LO] = (uint32_t)(r->seed & 0xffffffffu);
+  ew[HWY_E_SEED_HI] = (uint32_t)(r->seed >> 32);
+  ew[HWY_E_EGO_ACC] = hm_f2bits(r->v[0].act_acc);
+  ew[HWY_E_EGO_STEER] = hm_f2bits(r->v[0].act_steer);
+  ew[HWY_E_RETURN] = hm_f2bits(r->ep_return);
+}
+
+/* ------------------------------------------------------------------ road geometry */
+/* StraightLane.local_coordinates on lane c of straight_road_network: start (0, 4c), dir (1, 0) */
+static inline float lane_s(float x) { return x; }
+static inline float lane_lat(float y, int c) { return y - (float)c * LANE_WIDTH; }
+
+/* AbstractLane.on_lane(position, margin) */
+static int on_lane(float x, float y, int c, float margin) {
+  float s = lane_s(x), lat = lane_lat(y, c);
+  return hm_absf(lat) <= LANE_WIDTH / 2.0f + margin && -LANE_VEH_LEN <= s &&
+         s < ROAD_LENGTH + LANE_VEH_LEN;
+}
+
+/* AbstractLane.is_reachable_from */
+static int is_reachable_from(float x, float y, int c) {
+  float s = lane_s(x), lat = lane_lat(y, c);
+  return hm_absf(lat) <= 2.0f * LANE_WIDTH && 0.0f <= s && s < ROAD_LENGTH + LANE_VEH_LEN;
+}
+
+/* RoadNetwork.get_closest_lane_index: argmin over lanes of |lateral| (+ terms equal for all
+ * lanes of the straight road), first index wins ties. */
+static int closest_lane(float y, int lanes) {
+  int best = 0;
+  float bd = hm_absf(lane_lat(y, 0));
+  for (int c = 1; c < lanes; ++c) {
+    float d = hm_absf(lane_lat(y, c));
+    if (d < bd) {
+      bd = d;
+      best = c;
+    }
+  }
+  return best;
+}
+
+/* Road.neighbour_vehicles(vehicle, lane_index) */
+static void neighbour_vehicles(const Road* r, int self, int c, int* front, int* rear) {
+  float s = lane_s(r->v[self].x);
+  int fi = -1, ri = -1;
+  float s_front = 0.0f, s_rear = 0.0f;
+  for (int k = 0; k < r->V; ++k) {
+    if (k == self || !r->v[k].present) continue;
+    float s_v = lane_s(r->v[k].x);
+    if (!on_lane(r->v[k].x, r->v[k].y, c, 1.0f)) continue;
+    if (s <= s_v && (fi < 0 || s_v <= s_front)) {
+      s_front = s_v;
+      fi = k;
+    }
+    if (s_v < s && (ri < 0 || s_v > s_rear)) {
+      s_rear = s_v;
+      ri = k;
+    }
+  }
+  *front = fi;
+  *rear = ri;
+}
+
+/* ------------------------------------------------------------------ IDM / MOBIL (behavior.py) */
+/* IDMVehicle.desired_gap(ego_vehicle, front_vehicle, projected=True) */
+static float desired_gap(const Road* r, int ev, int fv) {
+  const Veh* a = &r->v[ev];
+  const Veh* b = &r->v[fv];
+  float ca = hm_cosf(a->heading), sa = hm_sinf(a->heading);
+  float cb = hm_cosf(b->heading), sb = hm_sinf(b->heading);
+  float avx = a->speed * ca, avy = a->speed * sa;
+  float bvx = b->speed * cb, bvy = b->speed * sb;
+  float dv = (avx - bvx) * ca + (avy - bvy) * sa;
+  return (DISTANCE_WANTED + a->speed * TIME_WANTED) + (a->speed * dv) / TWO_SQRT_AB;
+}
+
+/* IDMVehicle.acceleration(ego_vehicle, front_vehicle) evaluated with self.DELTA of `self` */
+static float idm_acceleration(const Road* r, int self, int ev, int fv) {
+  if (ev < 0) return 0.0f;
+  const Veh* e = &r->v[ev];
+  float tsp = (ev == 0) ? 0.0f : e->target_speed; /* plain Vehicle has no target_speed */
+  tsp = hm_clipf(tsp, 0.0f, r->cfg->speed_limit);
+  float base = hm_maxf(e->speed, 0.0f) / hm_absf(hm_not_zero(tsp));
+  float acc = COMFORT_ACC_MAX * (1.0f - hm_powf(base, r->v[self].delta));
+  if (fv >= 0) {
+    float d = lane_s(r->v[fv].x) - lane_s(e->x); /* lane_distance_to */
+    float g = desired_gap(r, ev, fv) / hm_not_zero(d);
+    acc = acc - COMFORT_ACC_MAX * (g * g);
+  }
+  return acc;
+}
+
+/* IDMVehicle.mobil(lane_index) */
+static int mobil(const Road* r, int self, int c) {
+  int new_preceding, new_following;
+  neighbour_vehicles(r, self, c, &new_preceding, &new_following);
+  float new_following_a = idm_acceleration(r, self, new_following, new_preceding);
+  float new_following_pred_a = idm_acceleration(r, self, new_following, self);
+  if (new_following_pred_a < -LANE_CHANGE_MAX_BRAKING_IMPOSED) return 0;
+  int old_preceding, old_following;
+  neighbour_vehicles(r, self, r->v[self].lane, &old_preceding, &old_following);
+  float self_pred_a = idm_acceleration(r, self, self, new_preceding);
+  /* route is None -> acceleration-advantage branch */
+  float self_a = idm_acceleration(r, self, self, old_preceding);
+  float old_following_a = idm_acceleration(r, self, old_following, self);
+  float old_following_pred_a = idm_acceleration(r, self, old_following, old_preceding);
+  float jerk = (self_pred_a - self_a) +
+               POLITENESS * (((new_following_pred_a - new_following_a) + old_following_pred_a) -
+                             old_following_a);
+  if (jerk < LANE_CHANGE_MIN_ACC_GAIN) return 0;
+  return 1;
+}
+
+/* IDMVehicle.change_lane_policy */
+static void change_lane_policy(Road* r, int self) {
+  Veh* me = &r->v[self];
+  if (me->lane != me->target_lane) {
+    /* abort if someone else is already changing into the same lane */
+    for (int k = 0; k < r->V; ++k) {
+      const Veh* v = &r->v[k];
+      if (k == self || !v->present) continue;
+      if (v->lane != me->target_lane && k != 0 /* isinstance ControlledVehicle */ &&
+          v->target_lane == me->target_lane) {
+        float d = lane_s(v->x) - lane_s(me->x);
+        float d_star = desired_gap(r, self, k);
+        if (0.0f < d && d < d_star) {
+          me->target_lane = me->lane;
+          break;
+        }
+      }
+    }
+    return;
+  }
+  if (!(LANE_CHANGE_DELAY < me->timer)) return; /* utils.do_every */
+  me->timer = 0.0f;
+  int lanes = r->cfg->lanes_count;
+  int cand[2], nc = 0;
+  if (me->lane > 0) cand[nc++] = me->lane - 1; /* RoadNetwork.side_lanes */
+  if (me->lane < lanes - 1) cand[nc++] = me->lane + 1;
+  for (int q = 0; q < nc; ++q) {
+    int c = cand[q];
+    if (!is_reachable_from(me->x, me->y, c)) continue;
+    if (hm_absf(me->speed) < 1.0f) continue;
+    if (mobil(r, self, c)) me->target_lane = c;
+  }
+}
+
+/* ControlledVehicle.steering_control(target_lane_index) */
+static float steering_control(const Road* r, int self, int c) {
+  const Veh* me = &r->v[self];
+  float lat = lane_lat(me->y, c);
+  float lane_future_heading = 0.0f;
+  float lateral_speed_command = -KP_LATERAL * lat;
+  float heading_command = hm_asinf(hm_clipf(lateral_speed_command / hm_not_zero(me->speed), -1.0f, 1.0f));
+  float heading_ref = lane_future_heading + hm_clipf(heading_command, -HM_PIO4_F, HM_PIO4_F);
+  float heading_rate_command = KP_HEADING * hm_wrap_to_pi(heading_ref - me->heading);
+  float slip_angle = hm_asinf(hm_clipf((VEH_LENGTH / 2.0f) / hm_not_zero(me->speed) * heading_rate_command, -1.0f, 1.0f));
+  float steering_angle = hm_atanf(2.0f * hm_tanf(slip_angle));
+  return hm_clipf(steering_angle, -MAX_STEERING, MAX_STEERING);
+}
+
+/* IDMVehicle.act */
+static void idm_act(Road* r, int self) {
+  Veh* me = &r->v[self];
+  if (me->crashed) return;
+  change_lane_policy(r, self);
+  float steer = steering_control(r, self, me->target_lane);
+  steer = hm_clipf(steer, -MAX_STEERING, MAX_STEERING);
+  int front, rear;
+  neighbour_vehicles(r, self, me->lane, &front, &rear);
+  float acc = idm_acceleration(r, self, self, front);
+  if (me->lane != me->target_lane) {
+    neighbour_vehicles(r, self, me->target_lane, &front, &rear);
+    float target_idm_acceleration = idm_acceleration(r, self, self, front);
+    acc = hm_minf(acc, target_idm_acceleration);
+  }
+  acc = hm_clipf(acc, -ACC_MAX, ACC_MAX);
+  me->act_steer = steer;
+  me->act_acc = acc;
+}
+
+/* ------------------------------------------------------------------ kinematics.py */
+static void vehicle_step(Road* r, int i) {
+  Veh* v = &r->v[i];
+  float dt = r->dt;
+  if (i != 0) v->timer = v->timer + dt; /* IDMVehicle.step */
+  /* clip_actions */
+  if (v->crashed) {
+    v->act_steer = 0.0f;
+    v->act_acc = -1.0f * v->speed;
+  }
+  if (v->speed > MAX_SPEED) {
+    v->act_acc = hm_minf(v->act_acc, 1.0f * (MAX_SPEED - v->speed));
+  } else if (v->speed < MIN_SPEED) {
+    v->act_acc = hm_maxf(v->act_acc, 1.0f * (MIN_SPEED - v->speed));
+  }
+  float delta_f = v->act_steer;
+  float beta = hm_atanf(0.5f * hm_tanf(delta_f));
+  float vx = v->speed * hm_cosf(v->heading + beta);
+  float vy = v->speed * hm_sinf(v->heading + beta);
+  v->x = v->x + vx * dt;
+  v->y = v->y + vy * dt;
+  if (v->has_impact) {
+    v->x = v->x + v->imp_x;
+    v->y = v->y + v->imp_y;
+    v->crashed = 1;
+    v->has_impact = 0;
+  }
+  v->heading = v->heading + v->speed * hm_sinf(beta) / (VEH_LENGTH / 2.0f) * dt;
+  v->speed = v->speed + v->act_acc * dt;
+  v->lane = closest_lane(v->y, r->cfg->lanes_count); /* on_state_update */
+}
+
+/* ------------------------------------------------------------------ objects.py / utils.py */
+static void polygon(const Veh* v, float P[5][2]) {
+  const float px[4] = {-VEH_LENGTH / 2.0f, -VEH_LENGTH / 2.0f, VEH_LENGTH / 2.0f, VEH_LENGTH / 2.0f};
+  const float py[4] = {-VEH_WIDTH / 2.0f, VEH_WIDTH / 2.0f, VEH_WIDTH / 2.0f, -VEH_WIDTH / 2.0f};
+  float c = hm_cosf(v->heading), s = hm_sinf(v->heading);
+  for (int k = 0; k < 4; ++k) {
+    P[k][0] = (c * px[k] - s * py[k]) + v->x;
+    P[k][1] = (s * px[k] + c * py[k]) + v->y;
+  }
+  P[4][0] = P[0][0];
+  P[4][1] = P[0][1];
+}
+
+static void project_polygon(float P[5][2], float nx, float ny, float* mn, float* mx) {
+  int first = 1;
+  for (int k = 0; k < 5; ++k) {
+    float p = P[k][0] * nx + P[k][1] * ny;
+    if (first || p < *mn) *mn = p;
+    if (first || p > *mx) *mx = p;
+    first = 0;
+  }
+}
+
+static inline float interval_distance(float min_a, float max_a, float min_b, float max_b) {
+  return min_a < min_b ? min_b - max_a : min_a - max_b;
+}
+
+/* utils.are_polygons_intersecting(a, b, displacement_a, displacement_b) */
+static void are_polygons_intersecting(float A[5][2], float B[5][2], float dax, float day, float dbx,
+                                      float dby, int* intersecting, int* will_intersect, float* tx,
+                                      float* ty) {
+  int inter = 1, will = 1;
+  float min_distance = INFINITY, axx = 0.0f, axy = 0.0f;
+  float (*polys[2])[2] = {A, B};
+  for (int pi = 0; pi < 2; ++pi) {
+    float (*Q)[2] = polys[pi];
+    for (int k = 0; k < 4; ++k) {
+      float nx = -Q[k + 1][1] + Q[k][1];
+      float ny = Q[k + 1][0] - Q[k][0];
+      float nn = sqrtf(nx * nx + ny * ny);
+      nx = nx / nn;
+      ny = ny / nn;
+      float min_a, max_a, min_b, max_b;
+      project_polygon(A, nx, ny, &min_a, &max_a);
+      project_polygon(B, nx, ny, &min_b, &max_b);
+      if (interval_distance(min_a, max_a, min_b, max_b) > 0.0f) inter = 0;
+      float vp = nx * (dax - dbx) + ny * (day - dby);
+      if (vp < 0.0f)
+        min_a = min_a + vp;
+      else
+        max_a = max_a + vp;
+      float distance = interval_distance(min_a, max_a, min_b, max_b);
+      if (distance > 0.0f) will = 0;
+      if (!inter && !will) break;
+      if (hm_absf(distance) < min_distance) {
+        min_distance = hm_absf(distance);
+        float cax = ((A[0][0] + A[1][0]) + A[2][0]) + A[3][0];
+        float cay = ((A[0][1] + A[1][1]) + A[2][1]) + A[3][1];
+        float cbx = ((B[0][0] + B[1][0]) + B[2][0]) + B[3][0];
+        float cby = ((B[0][1] + B[1][1]) + B[2][1]) + B[3][1];
+        float dx = cax / 4.0f - cbx / 4.0f, dy = cay / 4.0f - cby / 4.0f;
+        if (dx * nx + dy * ny > 0.0f) {
+          axx = nx;
+          axy = ny;
+        } else {
+          axx = -nx;
+          axy = -ny;
+        }
+      }
+    }
+  }
+  *intersecting = inter;
+  *will_intersect = will;
+  *tx = will ? min_distance * axx : 0.0f;
+  *ty = will ? min_distance * axy : 0.0f;
+}
+
+/* RoadObject.handle_collisions(other, dt) with self = road.vehicles[i], other = [j], i < j */
+static void handle_collisions(Road* r, int i, int j) {
+  Veh* a = &r->v[i];
+  Veh* b = &r->v[j];
+  float dt = r->dt;
+  float dx = b->x - a->x, dy = b->y - a->y;
+  if (sqrtf(dx * dx + dy * dy) > (VEH_DIAGONAL + VEH_DIAGONAL) / 2.0f + a->speed * dt) return;
+  float A[5][2], B[5][2];
+  polygon(a, A);
+  polygon(b, B);
+  float dax = (a->speed * hm_cosf(a->heading)) * dt, day = (a->speed * hm_sinf(a->heading)) * dt;
+  float dbx = (b->speed * hm_cosf(b->heading)) * dt, dby = (b->speed * hm_sinf(b->heading)) * dt;
+  int inter, will;
+  float tx, ty;
+  are_polygons_intersecting(A, B, dax, day, dbx, dby, &inter, &will, &tx, &ty);
+  if (will) {
+    a->imp_x = tx / 2.0f;
+    a->imp_y = ty / 2.0f;
+    a->has_impact = 1;
+    b->imp_x = -tx / 2.0f;
+    b->imp_y = -ty / 2.0f;
+    b->has_impact = 1;
+  }
+  if (inter) {
+    a->crashed = 1;
+    b->crashed = 1;
+  }
+}
+
+/* ------------------------------------------------------------------ observation.py */
+static float feature_value(const Veh* v, int fid) {
+  switch (fid) {
+    case HWY_FEAT_PRESENCE: return 1.0f;
+    case HWY_FEAT_X: return v->x;
+    case HWY_FEAT_Y: return v->y;
+    case HWY_FEAT_VX: return v->speed * hm_cosf(v->heading);
+    case HWY_FEAT_VY: return v->speed * hm_sinf(v->heading);
+    case HWY_FEAT_COS_H: return hm_cosf(v->heading);
+    case HWY_FEAT_SIN_H: return hm_sinf(v->heading);
+    case HWY_FEAT_HEADING: return v->heading;
+  }
+  return 0.0f;
+}
+
+static int is_relative_feature(int fid) {
+  return fid == HWY_FEAT_X || fid == HWY_FEAT_Y || fid == HWY_FEAT_VX || fid == HWY_FEAT_VY;
+}
+
+/* wrappers applied on one observation [N, F] -> [N, F_out] (rope_embed.py / dist_embed.py /
+ * rank_embed.py).  dist_override: RotaryEmbedWrapper._apply_rope(obs, dist_norm) entry. */
+static void apply_pe(const float* in, float* out, int N, int F, int kind, int d, int ego_idx,
+                     float max_dist, const float* table, const float* dist_override) {
+  int Fo = F + ((kind == HWY_PE_RANK || kind == HWY_PE_DIST) ? d : 0);
+  for (int i = 0; i < N; ++i) {
+    const float* row = in + (size_t)i * F;
+    float* o = out + (size_t)i * Fo;
+    for (int f = 0; f < F; ++f) o[f] = row[f];
+    if (kind == HWY_PE_NONE) continue;
+    if (kind == HWY_PE_RANK) {
+      for (int k = 0; k < d; ++k) o[F + k] = table[(size_t)i * d + k];
+      continue;
+    }
+    float nd;
+    if (dist_override) {
+      nd = dist_override[i];
+    } else {
+      const float* eg = in + (size_t)ego_idx * F;
+      float rx = row[0] - eg[0], ry = row[1] - eg[1];
+      nd = hm_clipf(sqrtf(rx * rx + ry * ry) / max_dist, 0.0f, 1.0f);
+    }
+    if (kind == HWY_PE_DIST) {
+      int h = d / 2;
+      for (int k = 0; k < h; ++k) {
+        float ang = (HM_TWO_PI_F * nd) * table[k];
+        o[F + k] = hm_sinf(ang);
+        o[F + h + k] = hm_cosf(ang);
+      }
+    } else { /* rope: rotate pairs (2p, 2p+1), p < d/2 */
+      for (int p = 0; p < d / 2; ++p) {
+        float th = (HM_TWO_PI_F * nd) * table[p];
+        float s = hm_sinf(th), c = hm_cosf(th);
+        float x = row[2 * p], y = row[2 * p + 1];
+        o[2 * p] = x * c - y * s;
+        o[2 * p + 1] = x * s + y * c;
+      }
+    }
+  }
+}
+
+/* KinematicObservation.observe + the fused wrapper; obs is [N, F_out] */
+static void observe(const Road* r, float* obs, const float* pe_table) {
+  const hwy_config* cfg = r->cfg;
+  int N = cfg->obs_vehicles, F = cfg->n_features;
+  float raw[HWY_MAX_OBS_ROWS * HWY_MAX_FEATURES];
+  memset(raw, 0, sizeof(raw));
+  const Veh* ego = &r->v[0];
+  /* Road.close_objects_to(ego, PERCEPTION_DISTANCE, count=N-1, see_behind, sort) */
+  int close[HWY_MAX_VEHICLES], nclose = 0;
+  for (int k = 0; k < r->V; ++k) {
+    const Veh* v = &r->v[k];
+    if (k == 0 || !v->present) continue;
+    float dx = v->x - ego->x, dy = v->y - ego->y;
+    if (!(sqrtf(dx * dx + dy * dy) < PERCEPTION_DISTANCE)) continue;
+    if (!(cfg->see_behind || -2.0f * VEH_LENGTH < lane_s(v->x) - lane_s(ego->x))) continue;
+    close[nclose++] = k;
+  }
+  if (cfg->order == HWY_ORDER_SORTED) { /* stable insertion sort by |lane_distance_to| */
+    for (int a = 1; a < nclose; ++a) {
+      int k = close[a];
+      float key = hm_absf(lane_s(r->v[k].x) - lane_s(ego->x));
+      int b = a - 1;
+      while (b >= 0 && hm_absf(lane_s(r->v[close[b]].x) - lane_s(ego->x)) > key) {
+        close[b + 1] = close[b];
+        --b;
+      }
+      close[b + 1] = k;
+    }
+  }
+  int count = N - 1;
+  if (nclose > count) nclose = count;
+  /* rows: ego (absolute) then others (relative unless "absolute") */
+  for (int row = 0; row < 1 + nclose; ++row) {
+    const Veh* v = row == 0 ? ego : &r->v[close[row - 1]];
+    for (int f = 0; f < F; ++f) {
+      int fid = cfg->feature_ids[f];
+      float val = feature_value(v, fid);
+      if (row > 0 && !cfg->absolute && is_relative_feature(fid)) val = val - feature_value(ego, fid);
+      if (cfg->normalize && cfg->has_range[f]) {
+        val = hm_lmap(val, cfg->features_range[f][0], cfg->features_range[f][1], -1.0f, 1.0f);
+        if (cfg->clip) val = hm_clipf(val, -1.0f, 1.0f);
+      }
+      raw[row * F + f] = val;
+    }
+  }
+  if (cfg->order == HWY_ORDER_SHUFFLED && N > 2) { /* np_random.shuffle(obs[1:]) */
+    uint32_t key[HWY_MAX_OBS_ROWS];
+    uint32_t k0 = (uint32_t)(r->seed & 0xffffffffu), k1 = (uint32_t)(r->seed >> 32);
+    for (int q = 0; q < N - 1; ++q)
+      key[q] = hm_philox4x32_10((uint32_t)q, (uint32_t)r->step, 0u, 0x53485546u, k0, k1).v[0];
+    float tmp[HWY_MAX_OBS_ROWS * HWY_MAX_FEATURES];
+    memcpy(tmp, raw, sizeof(float) * N * F);
+    for (int q = 0; q < N - 1; ++q) {
+      int dest = 0;
+      for (int p = 0; p < N - 1; ++p)
+        if (key[p] < key[q] || (key[p] == key[q] && p < q)) ++dest;
+      for (int f = 0; f < F; ++f) raw[(1 + dest) * F + f] = tmp[(1 + q) * F + f];
+    }
+  }
+  apply_pe(raw, obs, N, F, cfg->pe_kind, cfg->d_embed, cfg->ego_idx, cfg->pe_max_dist, pe_table,
+           NULL);
+}
+
+/* ------------------------------------------------------------------ highway_env.py */
+static float exp_density_factor(int lanes) { return hm_expf((-5.0f / 40.0f) * (float)lanes); }
+
+/* HighwayEnv._create_vehicles with Vehicle.create_random / IDMVehicle.randomize_behavior */
+static void reset_road(Road* r, uint64_t seed, int episode) {
+  const hwy_config* cfg = r->cfg;
+  int lanes = cfg->lanes_count;
+  uint32_t k0 = (uint32_t)(seed & 0xffffffffu), k1 = (uint32_t)(seed >> 32);
+  float fac = exp_density_factor(lanes);
+  float max_x = 0.0f;
+  for (int i = 0; i < HWY_MAX_VEHICLES; ++i) memset(&r->v[i], 0, sizeof(Veh));
+  for (int i = 0; i < r->V; ++i) {
+    hm_u32x4 u = hm_philox4x32_10((uint32_t)i, 0u, 0u, 0x52535431u, k0, k1);
+    Veh* v = &r->v[i];
+    int lane;
+    float speed, spacing;
+    if (i == 0) {
+      lane = cfg->initial_lane_id >= 0 ? cfg->initial_lane_id : hm_choice(u.v[0], lanes);
+      speed = 25.0f;
+      spacing = cfg->ego_spacing;
+    } else {
+      lane = hm_choice(u.v[0], lanes);
+      speed = hm_uniform(u.v[1], 0.7f * cfg->speed_limit, 0.8f * cfg->speed_limit);
+      spacing = 1.0f / cfg->vehicles_density;
+    }
+    float default_spacing = 12.0f + 1.0f * speed;
+    float offset = spacing * default_spacing * fac;
+    float x0 = (i == 0) ? 3.0f * offset : max_x;
+    x0 = x0 + offset * hm_uniform(u.v[2], 0.9f, 1.1f);
+    v->x = x0;
+    v->y = (float)lane * LANE_WIDTH;
+    v->heading = 0.0f;
+    v->speed = speed;
+    v->lane = lane;
+    v->target_lane = lane;
+    v->target_speed = speed;
+    v->present = 1;
+    if (i == 0) {
+      v->delta = 0.0f;
+      v->timer = 0.0f;
+    } else {
+      float t = (v->x + v->y) * HM_PI_F;
+      v->timer = t - hm_floorf(t); /* % LANE_CHANGE_DELAY */
+      v->delta = hm_uniform(u.v[3], 3.5f, 4.5f);
+    }
+    if (i == 0 || x0 > max_x) max_x = x0;
+  }
+  r->step = 0;
+  r->episode = episode;
+  r->seed = seed;
+  r->ep_return = 0.0f;
+}
+
+/* HighwayEnv._rewards / _reward */
+static float reward_of(const Road* r, int* on_road_out) {
+  const hwy_config* cfg = r->cfg;
+  const Veh* ego = &r->v[0];
+  int lane = ego->lane;
+  float forward_speed = ego->speed * hm_cosf(ego->heading);
+  float scaled_speed = hm_lmap(forward_speed, cfg->reward_speed_range[0], cfg->reward_speed_range[1], 0.0f, 1.0f);
+  float collision = ego->crashed ? 1.0f : 0.0f;
+  int nl = cfg->lanes_count - 1;
+  float right_lane = (float)lane / (float)(nl > 1 ? nl : 1);
+  float high_speed = hm_clipf(scaled_speed, 0.0f, 1.0f);
+  int on_road = on_lane(ego->x, ego->y, lane, 0.0f);
+  float on_road_f = on_road ? 1.0f : 0.0f;
+  float rew = 0.0f;
+  rew = rew + cfg->collision_reward * collision;
+  rew = rew + cfg->right_lane_reward * right_lane;
+  rew = rew + cfg->high_speed_reward * high_speed;
+  rew = rew + cfg->on_road_reward * on_road_f;
+  if (cfg->normalize_reward)
+    rew = hm_lmap(rew, cfg->collision_reward, cfg->high_speed_reward + cfg->right_lane_reward, 0.0f, 1.0f);
+  rew = rew * on_road_f;
+  *on_road_out = on_road;
+  return rew;
+}
+
+static uint64_t schedule_seed(const hwy_config* cfg, int e, int episode) {
+  return (uint64_t)(cfg->seed_base + (int64_t)cfg->env_offset + (int64_t)e + 1 +
+                    cfg->seed_stride * (int64_t)episode);
+}
+
+/* AbstractEnv.step: time += 1/policy_frequency; _simulate(action); observe; reward; flags */
+static void step_road(Road* r, const float* action, float* obs, float* reward, uint8_t* term,
+                      uint8_t* trunc, float* ep_ret, int32_t* ep_len, const float* pe_table, int e) {
+  const hwy_config* cfg = r->cfg;
+  int frames = cfg->sim_freq / cfg->policy_freq;
+  for (int frame = 0; frame < frames; ++frame) {
+    if (frame == 0) { /* ContinuousAction.act -> ego.act(get_action(action)) */
+      float a0 = hm_clipf(action[0], -1.0f, 1.0f), a1 = hm_clipf(action[1], -1.0f, 1.0f);
+      r->v[0].act_acc = hm_lmap(a0, -1.0f, 1.0f, -5.0f, 5.0f);
+      r->v[0].act_steer = hm_lmap(a1, -1.0f, 1.0f, -HM_PIO4_F, HM_PIO4_F);
+    }
+    for (int i = 1; i < r->V; ++i) /* Road.act (ego keeps its action) */
+      if (r->v[i].present) idm_act(r, i);
+    for (int i = 0; i < r->V; ++i) /* Road.step */
+      if (r->v[i].present) vehicle_step(r, i);
+    for (int i = 0; i < r->V; ++i)
+      for (int j = i + 1; j < r->V; ++j)
+        if (r->v[i].present && r->v[j].present) handle_collisions(r, i, j);
+  }
+  r->step += 1;
+  int on_road;
+  float rew = reward_of(r, &on_road);
+  int terminated = r->v[0].crashed || (cfg->offroad_terminal && !on_road);
+  int truncated = r->step >= cfg->max_steps;
+  r->ep_return = r->ep_return + rew;
+  *reward = rew;
+  *term = (uint8_t)terminated;
+  *trunc = (uint8_t)truncated;
+  int done = terminated || truncated;
+  if (ep_ret) *ep_ret = done ? r->ep_return : 0.0f;
+  if (ep_len) *ep_len = done ? r->step : 0;
+  if (done && cfg->autoreset) {
+    int k = r->episode + 1;
+    reset_road(r, schedule_seed(cfg, e, k), k);
+  }
+  observe(r, obs, pe_table);
+}
+
+/* ================================================================== exported oracle ABI */
+static int obs_fout(const hwy_config* cfg) {
+  return cfg->n_features +
+         ((cfg->pe_kind == HWY_PE_RANK || cfg->pe_kind == HWY_PE_DIST) ? cfg->d_embed : 0);
+}
+
+int hwyo_reset(const hwy_config* cfg, uint32_t* state, const uint64_t* seeds, const uint8_t* mask,
+               float* obs, const float* pe_table) {
+  int E = cfg->num_envs, stride = cfg->obs_vehicles * obs_fout(cfg);
+  Road r;
+  for (int e = 0; e < E; ++e) {
+    if (mask && !mask[e]) continue;
+    r.cfg = cfg;
+    r.V = cfg->vehicles_count + 1;
+    r.dt = 1.0f / (float)cfg->sim_freq;
+    uint64_t seed = seeds ? seeds[e] : schedule_seed(cfg, e, 0);
+    reset_road(&r, seed, 0);
+    store_road(&r, state, E, e);
+    if (obs) observe(&r, obs + (size_t)e * stride, pe_table);
+  }
+  return 0;
+}
+
+int hwyo_step(const hwy_config* cfg, uint32_t* state, const float* actions, float* obs,
+              float* reward, uint8_t* term, uint8_t* trunc, float* ep_ret, int32_t* ep_len,
+              const float* pe_table) {
+  int E = cfg->num_envs, stride = cfg->obs_vehicles * obs_fout(cfg);
+  Road r;
+  for (int e = 0; e < E; ++e) {
+    load_road(&r, cfg, state, E, e);
+    step_road(&r, actions + 2 * (size_t)e, obs + (size_t)e * stride, reward + e, term + e,
+              trunc + e, ep_ret ? ep_ret + e : NULL, ep_len ? ep_len + e : NULL, pe_table, e);
+    store_road(&r, state, E, e);
+  }
+  return 0;
+}
+
+/* observation of the current state without stepping (tests) */
+int hwyo_observe(const hwy_config* cfg, uint32_t* state, float* obs, const float* pe_table) {
+  int E = cfg->num_envs, stride = cfg->obs_vehicles * obs_fout(cfg);
+  Road r;
+  for (int e = 0; e < E; ++e) {
+    load_road(&r, cfg, state, E, e);
+    observe(&r, obs + (size_t)e * stride, pe_table);
+  }
+  return 0;
+}
+
+int hwyo_obs_pe(const float* obs_in, float* obs_out, int E, int N, int F, int kind, int d,
+                int ego_idx, float max_dist, const float* table, const float* dist_override) {
+  int Fo = F + ((kind == HWY_PE_RANK || kind == HWY_PE_DIST) ? d : 0);
+  for (int e = 0; e < E; ++e)
+    apply_pe(obs_in + (size_t)e * N * F, obs_out + (size_t)e * N * Fo, N, F, kind, d, ego_idx,
+             max_dist, table, dist_override ? dist_override + (size_t)e * N : NULL);
+  return 0;
+}
+
+/* PPOMemory.compute_advantages (ppo/agent.py:126-138) on a [T, E] rollout:
+ *   delta = r[t] + gamma * v[t+1] * (1 - d[t]) - v[t]            (float64)
+ *   adv[t] = float32(delta + gamma * lam * (1 - d[t]) * adv[t+1]) (float32 storage)
+ *   ret = adv + v (float32) */
+int hwyo_gae(const float* rew, const uint8_t* done, const float* val, const float* last_val,
+             double gamma, double lam, int T, int E, float* adv, float* ret) {
+  double gl = gamma * lam;
+  for (int e = 0; e < E; ++e) {
+    float last_adv = 0.0f;
+    for (int t = T - 1; t >= 0; --t) {
+      size_t i = (size_t)t * E + e;
+      double v1 = (t == T - 1) ? (double)last_val[e] : (double)val[i + E];
+      double nd = done[i] ? 0.0 : 1.0;
+      double delta = ((double)rew[i] + (gamma * v1) * nd) - (double)val[i];
+      float a = (float)(delta + (gl * nd) * (double)last_adv);
+      adv[i] = a;
+      ret[i] = a + val[i];
+      last_adv = a;
+    }
+  }
+  return 0;
+}
+
+/* math library on the host (tests compare against the device build bit for bit) */
+int hwyo_math(int op, const float* in, const float* in2, float* out, int n) {
+  for (int i = 0; i < n; ++i) {
+    float x = in[i], y = in2 ? in2[i] : 0.0f;
+    float r = 0.0f;
+    switch (op) {
+      case 0: r = hm_sinf(x); break;
+      case 1: r = hm_cosf(x); break;
+      case 2: r = hm_tanf(x); break;
+      case 3: r = hm_atanf(x); break;
+      case 4: r = hm_asinf(x); break;
+      case 5: r = hm_expf(x); break;
+      case 6: r = hm_logf(x); break;
+      case 7: r = hm_powf(x, y); break;
+      case 8: r = hm_wrap_to_pi(x); break;
+      case 9: r = sqrtf(x); break;
+      case 10: r = x / y; break;
+      case 11: r = hm_floorf(x); break;
+      default: return -1;
+    }
+    out[i] = r;
+  }
+  return 0;
+}
+
+/* Philox known-answer check helper */
+void hwyo_philox(const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
+  hm_u32x4 o = hm_philox4x32_10(ctr[0], ctr[1], ctr[2], ctr[3], key[0], key[1]);
+  for (int i = 0; i < 4; ++i) out[i] = o.v[i];
+}

@@ -1,0 +1,96 @@
+"""Device math library, stand-alone PE kernel and GAE kernel vs the CPU oracle (bit-exact)."""
+
+import numpy as np
+import pytest
+import torch
+
+from hwy import _abi, ops
+from oracle import oracle
+from parity_util import pe_table_for
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _inputs(op, rng, n=200000):
+    if op in (0, 1, 2, 8, 11):
+        x = np.concatenate([rng.uniform(-4, 4, n // 2), rng.uniform(-2000, 2000, n // 2)])
+    elif op == 3:
+        x = np.concatenate([rng.uniform(-3, 3, n // 2), rng.normal(0, 1e3, n // 2)])
+    elif op == 4:
+        x = rng.uniform(-1, 1, n)
+    elif op == 5:
+        x = rng.uniform(-110, 95, n)
+    elif op in (6, 9):
+        x = np.abs(rng.normal(0, 100, n)) + 1e-30
+    elif op == 7:
+        x = np.abs(rng.uniform(0, 4000, n))
+    else:
+        x = rng.normal(0, 100, n)
+    y = None
+    if op == 7:
+        y = rng.uniform(-4.5, 4.5, n)
+    if op == 10:
+        y = rng.normal(0, 10, n)
+    return x.astype(np.float32), None if y is None else y.astype(np.float32)
+
+
+@pytest.mark.parametrize("op", list(range(12)))
+def test_math_library_bit_exact(op):
+    rng = np.random.default_rng(op)
+    x, y = _inputs(op, rng)
+    host = oracle.math_op(op, x, y)
+    xt = torch.as_tensor(x, device=DEV)
+    yt = None if y is None else torch.as_tensor(y, device=DEV)
+    dev = ops.math_selftest(op, xt, yt).cpu().numpy()
+    bad = np.nonzero(host.view(np.uint32) != dev.view(np.uint32))[0]
+    assert bad.size == 0, f"op {op}: {bad.size} mismatches, e.g. x={x[bad[0]]!r} host={host[bad[0]]!r} dev={dev[bad[0]]!r}"
+
+
+@pytest.mark.parametrize("kind,d", [(_abi.PE_NONE, 0), (_abi.PE_ROPE, 4), (_abi.PE_ROPE, 2),
+                                    (_abi.PE_DIST, 4), (_abi.PE_DIST, 8), (_abi.PE_RANK, 4),
+                                    (_abi.PE_RANK, 3)])
+@pytest.mark.parametrize("ego_idx", [0, 2])
+def test_obs_pe_kernel_matches_oracle(kind, d, ego_idx):
+    rng = np.random.default_rng(kind * 10 + d)
+    E, N, F = 300, 15, 4
+    obs = rng.uniform(-1, 1, size=(E, N, F)).astype(np.float32)
+    obs[:, 10:] = 0.0  # zero-padded rows
+    table = pe_table_for(kind, d, N, seed=1)
+    want = oracle.obs_pe(obs, kind, d, ego_idx, 100.0, table)
+    tt = None if table is None else torch.as_tensor(table, device=DEV)
+    got = ops.obs_pe(torch.as_tensor(obs, device=DEV), kind, d, ego_idx, 100.0, tt).cpu().numpy()
+    np.testing.assert_array_equal(got, want)
+
+
+def test_obs_pe_dist_override():
+    rng = np.random.default_rng(0)
+    obs = rng.normal(size=(5, 6, 4)).astype(np.float32)
+    dn = rng.uniform(-1, 1, size=(5, 6)).astype(np.float32)
+    table = pe_table_for(_abi.PE_ROPE, 4, 6)
+    want = oracle.obs_pe(obs, _abi.PE_ROPE, 4, 0, 1.0, table, dist_override=dn)
+    got = ops.obs_pe(torch.as_tensor(obs, device=DEV), _abi.PE_ROPE, 4, 0, 1.0,
+                     torch.as_tensor(table, device=DEV),
+                     dist_override=torch.as_tensor(dn, device=DEV)).cpu().numpy()
+    np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("T,E", [(1, 1), (7, 3), (64, 4096), (200, 33)])
+def test_gae_kernel_matches_oracle(T, E):
+    rng = np.random.default_rng(T * 1000 + E)
+    rew = rng.uniform(0, 1, size=(T, E)).astype(np.float32)
+    val = rng.normal(size=(T, E)).astype(np.float32)
+    done = (rng.random((T, E)) < 0.05).astype(np.uint8)
+    last = rng.normal(size=E).astype(np.float32)
+    a_o, r_o = oracle.gae(rew, done, val, last, 0.99, 0.95)
+    t = lambda a: torch.as_tensor(a, device=DEV)  # noqa: E731
+    a_h, r_h = ops.gae(t(rew), t(done), t(val), t(last), 0.99, 0.95)
+    np.testing.assert_array_equal(a_h.cpu().numpy(), a_o)
+    np.testing.assert_array_equal(r_h.cpu().numpy(), r_o)
+
+
+def test_cpu_tensor_rejected():
+    from hwy.native import HwyNativeError
+
+    with pytest.raises(HwyNativeError):
+        ops.obs_pe(torch.zeros(1, 3, 4), _abi.PE_ROPE, 4, 0, 100.0, None)

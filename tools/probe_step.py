@@ -1,0 +1,24 @@
+"""Quick timing probe of hwy_step / hwy_reset on one GPU (development aid)."""
+import sys, os, time
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "highway-rope-ppo_amd"))
+import torch
+from config.base_config import HIGHWAY_CONFIG
+from hwy.vec_env import HighwayVecEnv
+
+for E in [int(x) for x in (sys.argv[1:] or ["4096", "16384"])]:
+    env = HighwayVecEnv(HIGHWAY_CONFIG, num_envs=E, device="cuda:0", autoreset=True, seed_base=42)
+    env.reset()
+    a = torch.zeros(E, 2, device="cuda:0")
+    for _ in range(5):
+        env.step(a)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 50
+    s.record()
+    for _ in range(n):
+        a.uniform_(-0.3, 0.3)
+        env.step(a)
+    e.record(); torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / n
+    print(f"E={E}: {ms:.3f} ms/step  -> {E/ms*1e3/1e6:.2f} M env-steps/s", flush=True)
+    env.close()
