@@ -33,7 +33,9 @@ static int hip_fail(hipError_t e, const char* what) {
 }
 
 static int pe_extra(const hwy_config* c) {
-  return (c->pe_kind == HWY_PE_RANK || c->pe_kind == HWY_PE_DIST) ? c->d_embed : 0;
+  return (c->pe_kind == HWY_PE_RANK || c->pe_kind == HWY_PE_DIST || c->pe_kind == HWY_PE_DIST1)
+             ? c->d_embed
+             : 0;
 }
 
 static int validate(const hwy_config* c) {
@@ -72,6 +74,10 @@ static int validate(const hwy_config* c) {
         return fail(HWY_EINVAL, "DistanceEmbedWrapper requires even d_embed; got %d", c->d_embed);
       if (c->n_features < 2) return fail(HWY_EINVAL, "DistPE needs at least 2 features");
       break;
+    case HWY_PE_DIST1:
+      if (c->d_embed < 2 || c->d_embed % 2)
+        return fail(HWY_EINVAL, "DistanceEmbedWrapper requires even d_embed; got %d", c->d_embed);
+      break;
     case HWY_PE_ROPE:
       if (c->d_embed % 2 || c->d_embed > c->n_features || c->d_embed < 0)
         return fail(HWY_EINVAL, "rotate_dim must be even and <= %d; got %d", c->n_features,
@@ -91,6 +97,8 @@ static int validate(const hwy_config* c) {
 extern "C" {
 
 int hwy_abi_version(void) { return HWY_ABI_VERSION; }
+
+int hwy_config_size(void) { return (int)sizeof(hwy_config); }
 
 const char* hwy_last_error(void) { return g_err; }
 
@@ -146,7 +154,7 @@ int hwy_set_pe_table(hwy_handle* h, const float* table_host, int n) {
   const hwy_config& c = h->cfg;
   int need = 0;
   if (c.pe_kind == HWY_PE_RANK) need = c.obs_vehicles * c.d_embed;
-  if (c.pe_kind == HWY_PE_DIST) need = c.d_embed / 2;
+  if (c.pe_kind == HWY_PE_DIST || c.pe_kind == HWY_PE_DIST1) need = c.d_embed / 2;
   if (c.pe_kind == HWY_PE_ROPE) need = c.d_embed / 2;
   if (n != need) return fail(HWY_EINVAL, "pe table needs %d floats, got %d", need, n);
   if (n > HWY_MAX_PE_TABLE) return fail(HWY_EINVAL, "pe table too large (%d)", n);
@@ -224,11 +232,11 @@ int hwy_obs_pe(const float* obs_in, float* obs_out, int E, int N, int F, int kin
     return fail(HWY_EINVAL, "hwy_obs_pe: bad shape E=%d N=%d F=%d", E, N, F);
   if (kind == HWY_PE_ROPE && (d % 2 || d > F || d < 0))
     return fail(HWY_EINVAL, "rotate_dim must be even and <= %d; got %d", F, d);
-  if (kind == HWY_PE_DIST && (d % 2 || d < 2))
+  if ((kind == HWY_PE_DIST || kind == HWY_PE_DIST1) && (d % 2 || d < 2))
     return fail(HWY_EINVAL, "DistanceEmbedWrapper requires even d_embed; got %d", d);
   if ((kind == HWY_PE_DIST || kind == HWY_PE_ROPE) && F < 2)
     return fail(HWY_EINVAL, "distance wrappers need at least 2 features");
-  if (kind < HWY_PE_NONE || kind > HWY_PE_ROPE) return fail(HWY_EINVAL, "unknown pe kind %d", kind);
+  if (kind < HWY_PE_NONE || kind > HWY_PE_DIST1) return fail(HWY_EINVAL, "unknown pe kind %d", kind);
   if (ego_idx < 0 || ego_idx >= N) return fail(HWY_EINVAL, "ego_idx %d out of range", ego_idx);
   if (kind != HWY_PE_NONE && !table && !(kind == HWY_PE_ROPE && d == 0))
     return fail(HWY_EINVAL, "pe table is NULL");

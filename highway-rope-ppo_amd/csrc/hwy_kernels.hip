@@ -324,10 +324,10 @@ __device__ __forceinline__ void write_pe_row(const float* vals, int F, int kind,
     if (f < F) out[f] = vals[f];
   if (kind == HWY_PE_RANK) {
     for (int k = 0; k < d; ++k) out[F + k] = table[row * d + k];
-  } else if (kind == HWY_PE_DIST) {
+  } else if (kind == HWY_PE_DIST || kind == HWY_PE_DIST1) {
     float rx = vals[0] - ex0, ry = vals[1] - ex1;
-    float nd = have_override ? override_nd
-                             : hm_clipf(__builtin_sqrtf(rx * rx + ry * ry) / max_dist, 0.0f, 1.0f);
+    float dist = kind == HWY_PE_DIST ? __builtin_sqrtf(rx * rx + ry * ry) : hm_absf(rx);
+    float nd = have_override ? override_nd : hm_clipf(dist / max_dist, 0.0f, 1.0f);
     const int hd = d / 2;
     for (int k = 0; k < hd; ++k) {
       float ang = (HM_TWO_PI_F * nd) * table[k];
@@ -811,7 +811,7 @@ __global__ void __launch_bounds__(256) hwy_obs_pe_kernel(const float* __restrict
   if (t >= (long)E * N) return;
   const long e = t / N;
   const int r = (int)(t - e * N);
-  const int Fo = F + ((kind == HWY_PE_RANK || kind == HWY_PE_DIST) ? d : 0);
+  const int Fo = F + ((kind == HWY_PE_RANK || kind == HWY_PE_DIST || kind == HWY_PE_DIST1) ? d : 0);
   float vals[HWY_MAX_FEATURES];
 #pragma unroll
   for (int f = 0; f < HWY_MAX_FEATURES; ++f) vals[f] = f < F ? in[t * F + f] : 0.0f;

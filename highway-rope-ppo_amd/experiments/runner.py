@@ -1,0 +1,114 @@
+"""ExperimentRunner (reference experiments/runner.py:19-155) on the MI355X env.
+
+Same launch sequence and status dict: acquire device -> seed -> logger -> make_env ->
+``env.to(device)`` when the wrapper has it -> state/action dims -> PPOAgent ->
+train_with_experiment_name -> {"status": "COMPLETED"|"FAILED", ...}.  Experiment.extra may carry
+``num_envs`` (lockstep envs, > 1 selects the vectorised loop) and ``num_minibatches``.
+"""
+
+from __future__ import annotations
+
+import logging
+import time
+import traceback
+from typing import Any, Dict
+
+import numpy as np
+import torch
+
+from hwy.gym import spaces
+from ppo.agent import PPOAgent
+from training.routine import train_with_experiment_name
+from utils.logging_utils import setup_experiment_logger
+from utils.reproducibility import set_random_seeds
+
+from .config import Experiment
+from .wrappers import make_env
+
+
+class DevicePool:
+    """One HIP device per process (torch.distributed rank or LOCAL_RANK), not oversubscribed."""
+
+    def __init__(self, device: Any = None):
+        import os
+
+        if device is None and torch.cuda.is_available():
+            device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", 0)))
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+
+    def acquire(self):
+        import contextlib
+
+        @contextlib.contextmanager
+        def _cm():
+            yield self.device
+
+        return _cm()
+
+
+class ExperimentRunner:
+    def __init__(self, base_env_config: dict, device_pool=None):
+        self.base_config = base_env_config
+        self.pool = device_pool or DevicePool()
+
+    def _create_agent(self, state_dim, action_dim, hp, logger, device, extra=None):
+        extra = extra or {}
+        return PPOAgent(state_dim=state_dim, action_dim=action_dim, lr=hp.lr, gamma=hp.gamma,
+                        lam=hp.lam, eps_clip=hp.clip_eps, value_coef=hp.value_coef,
+                        entropy_coef=hp.entropy_coef, max_grad_norm=hp.max_grad_norm,
+                        epochs=hp.epochs, batch_size=hp.batch_size, hidden_dim=hp.hidden_dim,
+                        logger=logger, device=device,
+                        num_minibatches=extra.get("num_minibatches"))
+
+    def launch(self, exp: Experiment) -> Dict[str, Any]:
+        results: Dict[str, Any] = {"experiment_name": exp.name, "status": "FAILED"}
+        t0 = time.time()
+        logger = None
+        try:
+            with self.pool.acquire() as device:
+                set_random_seeds(exp.seed)
+                logger = setup_experiment_logger(exp.name)
+                logger.info(f"[{exp.name}] Acquired device: {device} | Seed: {exp.seed}")
+                logger.info(f"[{exp.name}] Condition: {exp.condition.name} | HPs: {exp.hp}")
+                env = None
+                try:
+                    overrides = dict(exp.env_config_overrides)
+                    if "num_envs" in exp.extra:
+                        overrides.setdefault("num_envs", exp.extra["num_envs"])
+                    if device.type == "cuda":
+                        overrides.setdefault("device", device)
+                    env = make_env(exp.condition, self.base_config, d_embed=exp.hp.d_embed,
+                                   env_overrides=overrides)
+                    if hasattr(env, "to") and callable(env.to):
+                        env = env.to(device)
+                    if not isinstance(env.observation_space, spaces.Box):
+                        raise TypeError(f"Unsupported observation space: {type(env.observation_space)}")
+                    state_dim = int(np.prod(env.observation_space.shape))
+                    action_dim = env.action_space.shape[0]
+                    logger.info(f"[{exp.name}] state_dim={state_dim}, action_dim={action_dim}")
+                    agent = self._create_agent(state_dim, action_dim, exp.hp, logger, device, exp.extra)
+                    rewards, avg_rewards, metrics = train_with_experiment_name(
+                        env=env, agent=agent, max_episodes=exp.max_episodes,
+                        target_reward=exp.target_reward,
+                        log_interval=exp.extra.get("log_interval", 20),
+                        eval_interval=exp.extra.get("eval_interval", 50),
+                        steps_per_update=exp.hp.steps_per_update, experiment_name=exp.name,
+                        exp_seed=exp.seed, logger=logger)
+                    results.update(status="COMPLETED", rewards=rewards, avg_rewards=avg_rewards,
+                                   metrics_history=metrics)
+                except Exception as e:
+                    logger.error(f"[{exp.name}] Experiment execution failed!", exc_info=True)
+                    results["error_message"] = str(e)
+                    results["error_traceback"] = traceback.format_exc()
+                finally:
+                    if env is not None:
+                        env.close()
+        except Exception as e:
+            results["error_message"] = str(e)
+            results["error_traceback"] = traceback.format_exc()
+        results["duration_seconds"] = time.time() - t0
+        if logger:
+            logger.info(f"[{exp.name}] Run finished. Status: {results['status']}. "
+                        f"Duration: {results['duration_seconds']:.2f}s")
+        logging.shutdown()
+        return results

@@ -29,7 +29,8 @@ FEATURES = {
     "heading": 7,
 }
 ORDER_SORTED, ORDER_SHUFFLED = 0, 1
-PE_NONE, PE_RANK, PE_DIST, PE_ROPE = 0, 1, 2, 3
+PE_NONE, PE_RANK, PE_DIST, PE_ROPE, PE_DIST1 = 0, 1, 2, 3, 4
+PE_APPENDS = (PE_RANK, PE_DIST, PE_DIST1)  # kinds that append d columns
 
 # enum hwy_field / hwy_env_word
 F_X, F_Y, F_HEADING, F_SPEED, F_TSPEED, F_DELTA, F_TIMER, F_IMPX, F_IMPY = range(9)
@@ -88,7 +89,7 @@ class HwyConfig(ctypes.Structure):
     ]
 
     def obs_features(self) -> int:
-        extra = self.d_embed if self.pe_kind in (PE_RANK, PE_DIST) else 0
+        extra = self.d_embed if self.pe_kind in PE_APPENDS else 0
         return int(self.n_features + extra)
 
     def as_dict(self) -> Dict[str, Any]:

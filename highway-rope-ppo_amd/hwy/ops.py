@@ -10,10 +10,10 @@ from typing import Optional, Tuple
 
 import torch
 
-from ._abi import PE_DIST, PE_NONE, PE_RANK, PE_ROPE
+from ._abi import PE_APPENDS, PE_DIST, PE_DIST1, PE_NONE, PE_RANK, PE_ROPE
 from .native import check, lib, ptr, require_device, stream_ptr
 
-__all__ = ["obs_pe", "gae", "math_selftest", "PE_NONE", "PE_RANK", "PE_DIST", "PE_ROPE"]
+__all__ = ["obs_pe", "gae", "math_selftest", "PE_NONE", "PE_RANK", "PE_DIST", "PE_ROPE", "PE_DIST1"]
 
 
 def obs_pe(obs: torch.Tensor, kind: int, d: int, ego_idx: int = 0, max_dist: float = 100.0,
@@ -28,7 +28,7 @@ def obs_pe(obs: torch.Tensor, kind: int, d: int, ego_idx: int = 0, max_dist: flo
     E = 1
     for s in lead:
         E *= int(s)
-    Fo = F + (d if kind in (PE_RANK, PE_DIST) else 0)
+    Fo = F + (d if kind in PE_APPENDS else 0)
     out = torch.empty(*lead, N, Fo, device=obs.device, dtype=torch.float32)
     if table is not None:
         require_device(table, "table")

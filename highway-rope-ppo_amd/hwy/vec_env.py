@@ -131,6 +131,14 @@ class HighwayVecEnv:
         self._alloc_buffers()
         self._set_obs_space()
 
+    def set_pe_table(self, table: np.ndarray) -> None:
+        """Replace the fused wrapper's table (e.g. RankEmbedWrapper.to(device))."""
+        t = np.ascontiguousarray(table, np.float32)
+        torch.cuda.synchronize(self.device)
+        check(lib().hwy_set_pe_table(self._handle, t.ctypes.data_as(ctypes.c_void_p), int(t.size)),
+              "hwy_set_pe_table")
+        self._pe_table = t
+
     # ------------------------------------------------------------------ API
     def reset(self, *, seed: Optional[int] = None, options: Optional[dict] = None,
               seeds: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None):

@@ -1,0 +1,471 @@
+"""PPO actor-critic for the MI355X build.
+
+API-compatible with the reference's ppo/agent.py:
+  * ActorCritic (:12-84): same module tree and parameter names (``shared.{0,2}``,
+    ``actor_mean.{0,2}``, ``log_std``, ``critic.{0,2}``) so checkpoints load both ways;
+    tanh-squashed Gaussian with the ``log1p(-a^2 + 1e-6)`` correction and the pre-tanh entropy.
+  * PPOMemory (:87-154): list memory with store / clear / compute_advantages / get_batches /
+    get_tensors; GAE runs in the HIP kernel (hwy_gae) with the reference's float64 arithmetic.
+  * PPOAgent (:157-327): same constructor, select_action, update(last_value), save / load and
+    the same metrics dict.
+
+MI355X additions (the batched hot path):
+  * ActorCritic.act(states) -- batched sampling on device, no host sync.
+  * RolloutBuffer -- device-resident [T, E] rollout storage written by the env kernel in place.
+  * PPOAgent.update_rollout(buffer, last_values) -- GAE kernel, global advantage normalisation,
+    one minibatch permutation reused for every epoch (ppo/agent.py:205), per-minibatch clipped
+    PPO step.  The step is captured once in a HIP graph and replayed; with a process group the
+    flat gradient bucket is all-reduced (RCCL) between the two captured halves.
+"""
+
+from __future__ import annotations
+
+import logging
+import math
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.distributions import Normal
+
+METRIC_KEYS = ("policy_loss", "value_loss", "entropy", "loss", "clip_fraction", "approx_kl")
+_LOG_SQRT_2PI = 0.5 * math.log(2 * math.pi)
+
+
+class ActorCritic(nn.Module):
+    """Shared 2-layer ReLU trunk, actor mean head + state-independent log_std, critic head."""
+
+    def __init__(self, state_dim: int, action_dim: int, hidden_dim: int = 128,
+                 device: torch.device = torch.device("cpu")):
+        super().__init__()
+        self.device = device
+        self.shared = nn.Sequential(
+            nn.Linear(state_dim, hidden_dim), nn.ReLU(),
+            nn.Linear(hidden_dim, hidden_dim), nn.ReLU(),
+        )
+        self.actor_mean = nn.Sequential(
+            nn.Linear(hidden_dim, hidden_dim), nn.ReLU(), nn.Linear(hidden_dim, action_dim)
+        )
+        self.log_std = nn.Parameter(torch.zeros(action_dim))
+        self.critic = nn.Sequential(
+            nn.Linear(hidden_dim, hidden_dim), nn.ReLU(), nn.Linear(hidden_dim, 1)
+        )
+        self.to(self.device)
+
+    def forward(self, x):
+        if isinstance(x, np.ndarray):
+            x = torch.as_tensor(x, dtype=torch.float32, device=self.device)
+        h = self.shared(x)
+        return self.actor_mean(h), self.log_std.exp(), self.critic(h)
+
+    @staticmethod
+    def squashed_log_prob(dist: Normal, z: torch.Tensor) -> torch.Tensor:
+        a = torch.tanh(z)
+        return (dist.log_prob(z) - torch.log1p(-a.pow(2) + 1e-6)).sum(dim=-1)
+
+    def get_action(self, state, deterministic: bool = False):
+        """Reference single-state API (numpy in, numpy / Python scalars out)."""
+        mean, std, value = self.forward(state)
+        if deterministic:
+            z = mean
+            log_prob = None
+        else:
+            dist = Normal(mean, std, validate_args=False)
+            z = dist.sample()
+            log_prob = self.squashed_log_prob(dist, z)
+        action = torch.tanh(z)
+        return (action.detach().cpu().numpy(), z.detach().cpu().numpy(),
+                None if log_prob is None else log_prob.item(),
+                value.detach().cpu().numpy()[0])
+
+    @torch.no_grad()
+    def act(self, states: torch.Tensor, deterministic: bool = False,
+            generator: Optional[torch.Generator] = None):
+        """Batched device sampling: returns (action, pre_tanh, log_prob, value) tensors."""
+        mean, std, value = self.forward(states)
+        if deterministic:
+            z = mean
+            logp = torch.zeros(mean.shape[0], device=mean.device)
+        else:
+            eps = torch.randn(mean.shape, device=mean.device, dtype=mean.dtype, generator=generator)
+            z = mean + std * eps
+            logp = self.squashed_log_prob(Normal(mean, std, validate_args=False), z)
+        return torch.tanh(z), z, logp, value.squeeze(-1)
+
+    def evaluate(self, states, actions, pre_tanh_actions):
+        mean, std, values = self.forward(states)
+        dist = Normal(mean, std, validate_args=False)  # no host-syncing argument checks
+        log_probs = self.squashed_log_prob(dist, pre_tanh_actions)
+        entropy = dist.entropy().sum(dim=-1)
+        return log_probs, values, entropy
+
+
+class PPOMemory:
+    """List-based rollout memory of the reference (one env, Python-side appends)."""
+
+    def __init__(self, batch_size: int = 64, device: torch.device = torch.device("cpu")):
+        self.batch_size = batch_size
+        self.device = device
+        self.clear()
+
+    def store(self, state, action, pre_tanh_action, reward, next_state, log_prob, done, value):
+        self.states.append(state)
+        self.actions.append(action)
+        self.pre_tanh_actions.append(pre_tanh_action)
+        self.rewards.append(reward)
+        self.next_states.append(next_state)
+        self.log_probs.append(log_prob)
+        self.dones.append(done)
+        self.values.append(value)
+
+    def clear(self):
+        self.states: List[Any] = []
+        self.actions: List[Any] = []
+        self.pre_tanh_actions: List[Any] = []
+        self.rewards: List[float] = []
+        self.next_states: List[Any] = []
+        self.log_probs: List[float] = []
+        self.dones: List[bool] = []
+        self.values: List[float] = []
+
+    def compute_advantages(self, gamma: float, lam: float, last_value: float):
+        """GAE of ppo/agent.py:126-138 on the HIP device (hwy_gae); returns numpy arrays."""
+        from hwy import ops
+        from hwy.native import HwyNativeError
+
+        dev = self.device if torch.device(self.device).type == "cuda" else (
+            torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else None)
+        if dev is None:
+            raise HwyNativeError("compute_advantages runs the HIP GAE kernel; no HIP device found")
+        T = len(self.rewards)
+        rew = torch.as_tensor(np.asarray(self.rewards, np.float32).reshape(T, 1), device=dev)
+        val = torch.as_tensor(np.asarray(self.values, np.float32).reshape(T, 1), device=dev)
+        done = torch.as_tensor(np.asarray(self.dones, np.uint8).reshape(T, 1), device=dev)
+        last = torch.tensor([float(last_value)], dtype=torch.float32, device=dev)
+        adv, ret = ops.gae(rew, done, val, last, gamma, lam)
+        return adv.view(T).cpu().numpy(), ret.view(T).cpu().numpy()
+
+    def get_batches(self):
+        n = len(self.states)
+        indices = np.arange(n, dtype=np.int64)
+        np.random.shuffle(indices)  # global numpy RNG, as ppo/agent.py:143
+        return [indices[i:i + self.batch_size] for i in range(0, n, self.batch_size)]
+
+    def get_tensors(self):
+        dev = self.device
+        f = lambda xs: torch.as_tensor(np.array(xs), dtype=torch.float32, device=dev)  # noqa: E731
+        return f(self.states), f(self.actions), f(self.pre_tanh_actions), f(self.log_probs)
+
+
+class RolloutBuffer:
+    """Device-resident rollout of T steps x E envs (the env kernel writes rows in place)."""
+
+    def __init__(self, T: int, E: int, state_dim: int, action_dim: int, device: torch.device):
+        kw = dict(device=device, dtype=torch.float32)
+        self.T, self.E, self.state_dim = T, E, state_dim
+        self.states = torch.zeros(T + 1, E, state_dim, **kw)  # row T = bootstrap obs
+        self.pre_tanh = torch.zeros(T, E, action_dim, **kw)
+        self.actions = torch.zeros(T, E, action_dim, **kw)
+        self.log_probs = torch.zeros(T, E, **kw)
+        self.values = torch.zeros(T, E, **kw)
+        self.rewards = torch.zeros(T, E, **kw)
+        self.terminated = torch.zeros(T, E, device=device, dtype=torch.uint8)
+        self.truncated = torch.zeros(T, E, device=device, dtype=torch.uint8)
+        self.dones = torch.zeros(T, E, device=device, dtype=torch.uint8)
+        self.ep_return = torch.zeros(T, E, **kw)
+        self.ep_length = torch.zeros(T, E, device=device, dtype=torch.int32)
+
+    @property
+    def n(self) -> int:
+        return self.T * self.E
+
+
+class _Learner:
+    """Per-minibatch clipped-PPO step over a flattened device rollout, optionally graph-captured.
+
+    Semantics per minibatch (ppo/agent.py:216-262): ratio = exp(logp - old); kl = mean(ratio - 1
+    - log ratio); surrogate clipped at 1 +- eps; MSE value loss against returns; loss = pg +
+    vc*vf - ec*entropy; zero grad, backward, [all-reduce mean], clip_grad_norm_, Adam step.
+    Batch metrics land in a device buffer row per minibatch; nothing syncs with the host.
+    """
+
+    def __init__(self, agent: "PPOAgent", n: int, mb: int, n_steps: int, use_graph: bool,
+                 group=None):
+        self.agent = agent
+        ac = agent.actor_critic
+        dev = agent.device
+        self.params = [p for p in ac.parameters()]
+        numel = sum(p.numel() for p in self.params)
+        self.flat_grad = torch.zeros(numel, device=dev, dtype=torch.float32)
+        off = 0
+        for p in self.params:
+            p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        self.group = group
+        self.world = 1 if group is None else torch.distributed.get_world_size(group)
+        self.mb = mb
+        self.n = n
+        self.idx = torch.zeros(mb, dtype=torch.int64, device=dev)
+        self.metrics = torch.zeros(max(1, n_steps), len(METRIC_KEYS), device=dev)
+        self.row = torch.zeros((), dtype=torch.int64, device=dev)
+        self.src: Dict[str, torch.Tensor] = {}
+        self.use_graph = use_graph and dev.type == "cuda"
+        self.g_fwd = self.g_opt = None
+
+    def bind(self, states, pre_tanh, old_logp, adv, ret):
+        same = all(self.src.get(k) is v for k, v in (("s", states), ("z", pre_tanh),
+                                                      ("lp", old_logp), ("a", adv), ("r", ret)))
+        if not same:
+            self.src = dict(s=states, z=pre_tanh, lp=old_logp, a=adv, r=ret)
+            self.g_fwd = self.g_opt = None  # new storage -> recapture
+
+    def _fwd_bwd(self):
+        ag = self.agent
+        s = self.src["s"].index_select(0, self.idx)
+        z = self.src["z"].index_select(0, self.idx)
+        old = self.src["lp"].index_select(0, self.idx)
+        a = self.src["a"].index_select(0, self.idx)
+        r = self.src["r"].index_select(0, self.idx)
+        new_lp, values, ent = ag.actor_critic.evaluate(s, torch.tanh(z), z)
+        log_ratio = new_lp - old
+        ratios = torch.exp(log_ratio)
+        surr1 = ratios * a
+        surr2 = torch.clamp(ratios, 1 - ag.eps_clip, 1 + ag.eps_clip) * a
+        actor_loss = -torch.min(surr1, surr2).mean()
+        critic_loss = F.mse_loss(values.squeeze(-1), r)
+        ent_b = ent.mean()
+        loss = actor_loss + ag.value_coef * critic_loss - ag.entropy_coef * ent_b
+        self.flat_grad.zero_()
+        loss.backward()
+        with torch.no_grad():
+            kl = ((ratios - 1) - log_ratio).mean()
+            clip = (torch.abs(ratios - 1) > ag.eps_clip).float().sum()  # / size on the host
+            vals = torch.stack([actor_loss, critic_loss, ent_b, loss, clip, kl]).detach()
+            self.metrics.index_copy_(0, self.row.view(1), vals.view(1, -1))
+
+    def _opt(self):
+        ag = self.agent
+        nn.utils.clip_grad_norm_(self.params, ag.max_grad_norm, foreach=True)
+        ag.optimizer.step()
+        self.row.add_(1)
+
+    def _allreduce(self):
+        if self.group is not None:
+            torch.distributed.all_reduce(self.flat_grad, group=self.group)
+            self.flat_grad.div_(self.world)
+
+    def _capture(self):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):  # warm-up builds autograd / optimizer state eagerly
+            for _ in range(2):
+                self._fwd_bwd()
+                self._allreduce()
+                self._opt()
+        torch.cuda.current_stream().wait_stream(s)
+        self.g_fwd, self.g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_fwd):
+            self._fwd_bwd()
+        with torch.cuda.graph(self.g_opt):
+            self._opt()
+
+    def step(self, idx: torch.Tensor):
+        self.idx.copy_(idx)
+        if self.use_graph:
+            if self.g_fwd is None:
+                saved = [p.detach().clone() for p in self.params]
+                opt_state = {k: {kk: (vv.clone() if torch.is_tensor(vv) else vv)
+                                 for kk, vv in v.items()} for k, v in self.agent.optimizer.state.items()}
+                row = self.row.clone()
+                self._capture()
+                with torch.no_grad():  # undo the warm-up steps
+                    for p, v in zip(self.params, saved):
+                        p.copy_(v)
+                    for k, st in self.agent.optimizer.state.items():
+                        for kk, vv in st.items():
+                            if not torch.is_tensor(vv):
+                                continue
+                            if k in opt_state:
+                                vv.copy_(opt_state[k][kk])
+                            else:  # state created by the warm-up: back to a fresh Adam
+                                vv.zero_()
+                    self.row.copy_(row)
+            self.g_fwd.replay()
+            self._allreduce()
+            self.g_opt.replay()
+        else:
+            self._fwd_bwd()
+            self._allreduce()
+            self._opt()
+
+
+class PPOAgent:
+    def __init__(self, state_dim: int, action_dim: int, lr: float = 1e-4, gamma: float = 0.99,
+                 lam: float = 0.95, eps_clip: float = 0.2, value_coef: float = 0.5,
+                 entropy_coef: float = 0.005, max_grad_norm: float = 0.5, epochs: int = 6,
+                 batch_size: int = 64, hidden_dim: int = 128,
+                 logger: Optional[logging.Logger] = None,
+                 device: torch.device = torch.device("cpu"),
+                 num_minibatches: Optional[int] = None, use_graphs: bool = True,
+                 process_group=None, seed: Optional[int] = None):
+        self.device = torch.device(device)
+        self.actor_critic = ActorCritic(state_dim, action_dim, hidden_dim, device=self.device)
+        self._dist = process_group
+        if process_group is not None:  # identical initial weights on every rank
+            for p in self.actor_critic.parameters():
+                torch.distributed.broadcast(p.data, src=0, group=process_group)
+        capturable = self.device.type == "cuda"
+        self.optimizer = torch.optim.Adam(self.actor_critic.parameters(), lr=lr,
+                                          capturable=capturable)
+        self.gamma, self.lam, self.eps_clip = gamma, lam, eps_clip
+        self.value_coef, self.entropy_coef = value_coef, entropy_coef
+        self.max_grad_norm, self.epochs, self.batch_size = max_grad_norm, epochs, batch_size
+        self.num_minibatches = num_minibatches
+        self.use_graphs = use_graphs
+        self.logger = logger or logging.getLogger(__name__)
+        self.memory = PPOMemory(batch_size=batch_size, device=self.device)
+        self._learner: Optional[_Learner] = None
+        self.generator = None
+        if self.device.type == "cuda":
+            self.generator = torch.Generator(device=self.device)
+            self.generator.manual_seed(int(seed) if seed is not None else torch.initial_seed() % (2**63))
+
+    # ------------------------------------------------------------------ acting
+    def select_action(self, state, deterministic: bool = False):
+        if isinstance(state, torch.Tensor) and state.dim() == 2:
+            return self.actor_critic.act(state, deterministic, generator=self.generator)
+        return self.actor_critic.get_action(state, deterministic)
+
+    # ------------------------------------------------------------------ metrics
+    def _finish_metrics(self, rows: np.ndarray, sizes: List[int], values, returns) -> Dict[str, float]:
+        """Aggregate per-minibatch rows like ppo/agent.py:263-287 (epoch means, then the mean
+        over epochs, in float64) plus explained variance (:272-280)."""
+        nb = len(sizes)
+        totals = dict.fromkeys(METRIC_KEYS, 0.0)
+        ci = METRIC_KEYS.index("clip_fraction")
+        for e in range(self.epochs):
+            blk = rows[e * nb:(e + 1) * nb]
+            for j, k in enumerate(METRIC_KEYS):
+                s = 0.0
+                for b in range(nb):
+                    v = float(blk[b, j])
+                    s += v / sizes[b] if j == ci else v
+                totals[k] += s / nb
+        with torch.no_grad():
+            var_y = torch.var(returns)
+            ev = (1 - torch.var(returns - values) / var_y).item() if var_y.item() > 0 else 0.0
+        out = {
+            "loss": totals["loss"] / self.epochs,
+            "policy_loss": totals["policy_loss"] / self.epochs,
+            "value_loss": totals["value_loss"] / self.epochs,
+            "entropy": totals["entropy"] / self.epochs,
+            "clip_fraction": totals["clip_fraction"] / self.epochs,
+            "approx_kl": totals["approx_kl"] / self.epochs,
+            "explained_variance": ev,
+        }
+        self.logger.info(
+            "update_complete loss=%.4f policy_loss=%.4f value_loss=%.4f entropy=%.4f "
+            "clip_frac=%.3f kl=%.5f explained_var=%.3f", out["loss"], out["policy_loss"],
+            out["value_loss"], out["entropy"], out["clip_fraction"], out["approx_kl"], ev)
+        return out
+
+    def _learner_for(self, n: int, mb: int, steps: int, graph: bool) -> _Learner:
+        L = self._learner
+        if L is None or L.n != n or L.mb != mb or L.metrics.shape[0] != steps:
+            L = _Learner(self, n, mb, steps, graph, group=self._dist)
+            self._learner = L
+        return L
+
+    def _run_epochs(self, states, pre_tanh, old_logp, adv, ret, batches: List[torch.Tensor]):
+        n = states.shape[0]
+        sizes = {int(b.numel()) for b in batches}
+        mb = max(sizes)
+        ragged = len(sizes) > 1
+        steps = self.epochs * len(batches)
+        if ragged:  # short last minibatch (reference's n % batch_size != 0): eager, exact sizes
+            rows = []
+            for _ in range(self.epochs):
+                for b in batches:
+                    L = self._learner_for(n, int(b.numel()), 1, False)
+                    L.bind(states, pre_tanh, old_logp, adv, ret)
+                    L.row.zero_()
+                    L.step(b)
+                    rows.append(L.metrics[0].clone())
+            return torch.stack(rows)
+        L = self._learner_for(n, mb, steps, self.use_graphs)
+        L.bind(states, pre_tanh, old_logp, adv, ret)
+        L.row.zero_()
+        for _ in range(self.epochs):
+            for b in batches:
+                L.step(b)
+        return L.metrics
+
+    # ------------------------------------------------------------------ reference update
+    def update(self, last_value: float = 0.0):
+        """Clipped-PPO update over the list memory (ppo/agent.py:196-308)."""
+        states, actions, pre_tanh, old_log_probs = self.memory.get_tensors()
+        adv_np, ret_np = self.memory.compute_advantages(self.gamma, self.lam, last_value)
+        advantages = torch.as_tensor(adv_np, device=self.device)
+        returns = torch.as_tensor(ret_np, device=self.device)
+        advantages = (advantages - advantages.mean()) / (advantages.std() + 1e-8)
+        batches = [torch.as_tensor(b, device=self.device) for b in self.memory.get_batches()]
+        rows = self._run_epochs(states, pre_tanh, old_log_probs, advantages, returns, batches)
+        values = torch.as_tensor(np.asarray(self.memory.values, np.float32), device=self.device)
+        out = self._finish_metrics(rows.cpu().numpy(), [int(b.numel()) for b in batches], values,
+                                   returns)
+        self.memory.clear()
+        return out
+
+    # ------------------------------------------------------------------ batched update
+    def normalize_advantages(self, adv: torch.Tensor) -> torch.Tensor:
+        """(adv - mean) / (unbiased std + 1e-8) over ALL ranks' samples (ppo/agent.py:204)."""
+        if self._dist is None:
+            return (adv - adv.mean()) / (adv.std() + 1e-8)
+        a64 = adv.double()
+        stats = torch.stack([torch.tensor(float(adv.numel()), device=adv.device, dtype=torch.float64),
+                             a64.sum(), (a64 * a64).sum()])
+        torch.distributed.all_reduce(stats, group=self._dist)
+        n, s1, s2 = stats[0], stats[1], stats[2]
+        mean = s1 / n
+        var = (s2 - n * mean * mean) / (n - 1)
+        return ((adv - mean.float()) / (var.clamp_min(0).sqrt().float() + 1e-8))
+
+    def update_rollout(self, buf: RolloutBuffer, last_values: torch.Tensor,
+                       perm: Optional[torch.Tensor] = None, return_metrics: bool = True):
+        """Batched clipped-PPO update on a device rollout (no host round trips until the end)."""
+        from hwy import ops
+
+        T, E = buf.T, buf.E
+        adv, ret = ops.gae(buf.rewards, buf.dones, buf.values, last_values, self.gamma, self.lam)
+        n = T * E
+        states = buf.states[:T].reshape(n, -1)
+        pre_tanh = buf.pre_tanh.reshape(n, -1)
+        old_lp = buf.log_probs.reshape(n)
+        ret = ret.reshape(n)
+        adv = self.normalize_advantages(adv.reshape(n))
+        nmb = self.num_minibatches or max(1, n // self.batch_size)
+        if perm is None:
+            perm = torch.randperm(n, device=self.device, generator=self.generator)
+        mb = n // nmb
+        batches = [perm[i * mb:(i + 1) * mb] for i in range(nmb)]  # one partition, all epochs
+        rows = self._run_epochs(states, pre_tanh, old_lp, adv, ret, batches)
+        if not return_metrics:
+            return rows
+        return self._finish_metrics(rows.cpu().numpy(), [mb] * nmb, buf.values.reshape(n), ret)
+
+    # ------------------------------------------------------------------ checkpoints
+    def save(self, path: str):
+        torch.save({"model": self.actor_critic.state_dict(),
+                    "optimizer": self.optimizer.state_dict()}, path)
+        self.logger.info(f"model_saved path={path}")
+
+    def load(self, path: str, load_optimizer: bool = True):
+        ckpt = torch.load(path, map_location=self.device, weights_only=True)
+        self.actor_critic.load_state_dict(ckpt["model"])
+        if load_optimizer and "optimizer" in ckpt:
+            self.optimizer.load_state_dict(ckpt["optimizer"])
+        self._learner = None
+        self.logger.info(f"model_loaded path={path}")
+        return ckpt.get("config", {})

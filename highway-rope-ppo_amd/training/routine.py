@@ -1,0 +1,328 @@
+"""Training entry point (reference training/routine.py:14-297), on the MI355X env.
+
+``train_with_experiment_name`` keeps the reference's signature, return value
+``(rewards, avg_rewards, metrics_history)``, artifact names and schemas:
+  * artifacts/highway-ppo/checkpoints/ppo_highway_{best,solved}_<exp>.pth  (:104-107, :208-222)
+  * artifacts/highway-ppo/training_metrics_<exp>.json with the same keys  (:88-97, :246-251)
+  * artifacts/highway-ppo/summary_<exp>.csv, header
+    ``experiment,final_reward,max_reward,steps,best_model,plot``          (:282-295)
+  * artifacts/highway-ppo/ppo_highway_rewards_<exp>.png                    (:254-279)
+
+Two loops behind it:
+  * a one-env facade env (make_env default) runs the reference's loop as written: per-episode
+    ``env.reset(seed=exp_seed + episode_num)`` (:127), batch-1 select_action, list memory,
+    ``agent.update(last_value)`` every ``steps_per_update`` steps;
+  * a HighwayVecEnv (``num_envs`` > 1) runs E lockstep envs with in-kernel autoreset on the
+    same seed schedule (env e's k-th episode gets exp_seed + 1 + e + E*k, = exp_seed +
+    episode_num for E = 1), a device RolloutBuffer of T = ceil(steps_per_update / E) steps, and
+    ``agent.update_rollout``.  Episode bookkeeping (logging / eval every ``eval_interval``
+    completed episodes, best / solved checkpoints, moving average over the last 10 evals) follows
+    the reference, with completed episodes counted in env order within each step.
+``evaluate`` runs ``num_episodes`` deterministic episodes seeded exp_seed + 1000 + k (:14-29),
+as one batched env for the vectorised path.
+"""
+
+from __future__ import annotations
+
+import json
+import logging
+import math
+import os
+import time
+
+import numpy as np
+import torch
+
+from utils.logging_utils import ensure_artifacts_dir, setup_experiment_logger
+
+
+def _is_vector(env) -> bool:
+    return bool(getattr(env.unwrapped, "is_vector_env", False))
+
+
+def _flat_dim(env) -> int:
+    return int(np.prod(env.observation_space.shape))
+
+
+# ---------------------------------------------------------------------------------- evaluation
+def evaluate(env, agent, num_episodes=10, render=False, exp_seed: int = 0):
+    """Mean return of deterministic episodes seeded exp_seed + 1000 + k."""
+    if _is_vector(env):
+        return _evaluate_vector(env, agent, num_episodes, exp_seed)
+    totals = []
+    for ep in range(num_episodes):
+        state, _ = env.reset(seed=exp_seed + 1000 + ep)
+        flat = state.reshape(-1)
+        done, ep_reward = False, 0.0
+        while not done:
+            action, _, _, _ = agent.select_action(flat, deterministic=True)
+            nxt, reward, terminated, truncated, _ = env.step(action)
+            done = terminated or truncated
+            flat = nxt.reshape(-1)
+            ep_reward += reward
+        totals.append(ep_reward)
+    return float(np.mean(totals))
+
+
+def _eval_env_like(env, num_episodes: int):
+    """A num_episodes-wide copy of env (same config and fused wrapper), no autoreset."""
+    from hwy.vec_env import HighwayVecEnv
+
+    base = env.unwrapped
+    cfg = base.hwy_config
+    ev = HighwayVecEnv(base.config, num_envs=num_episodes, device=base.device, autoreset=False,
+                       pe_kind=cfg.pe_kind, d_embed=cfg.d_embed, ego_idx=cfg.ego_idx,
+                       pe_max_dist=cfg.pe_max_dist, pe_table=base._pe_table)
+    return ev
+
+
+def _evaluate_vector(env, agent, num_episodes, exp_seed):
+    cache = getattr(env.unwrapped, "_eval_envs", None)
+    if cache is None:
+        cache = {}
+        env.unwrapped._eval_envs = cache
+    ev = cache.get(num_episodes)
+    if ev is None:
+        ev = cache[num_episodes] = _eval_env_like(env, num_episodes)
+    dev = ev.device
+    seeds = torch.arange(num_episodes, device=dev, dtype=torch.int64) + (exp_seed + 1000)
+    obs, _ = ev.reset(seeds=seeds)
+    alive = torch.ones(num_episodes, dtype=torch.bool, device=dev)
+    total = torch.zeros(num_episodes, dtype=torch.float64, device=dev)
+    for _ in range(ev.max_episode_steps + 1):
+        a, _, _, _ = agent.select_action(obs.reshape(num_episodes, -1), deterministic=True)
+        obs, r, te, tr, _ = ev.step(a.contiguous())
+        total += torch.where(alive, r.double(), torch.zeros_like(total))
+        alive &= ~(te.bool() | tr.bool())
+        if not bool(alive.any()):
+            break
+    return float(total.mean().item())
+
+
+# ---------------------------------------------------------------------------------- artifacts
+def _save_artifacts(artifacts_dir, checkpoint_dir, experiment_name, metrics_history,
+                    training_episodes, episode_rewards, eval_episodes, rewards, avg_rewards,
+                    target_reward, total_steps, logger, exp_prefix):
+    metrics_path = os.path.join(artifacts_dir, f"training_metrics_{experiment_name}.json")
+    with open(metrics_path, "w") as f:
+        json.dump(metrics_history, f, indent=2)
+    logger.info(f"{exp_prefix} Metrics saved to {metrics_path}")
+    plot_path = os.path.join(artifacts_dir, f"ppo_highway_rewards_{experiment_name}.png")
+    try:
+        import matplotlib
+
+        matplotlib.use("Agg")
+        import matplotlib.pyplot as plt
+
+        plt.figure(figsize=(12, 8))
+        plt.plot(training_episodes, episode_rewards, alpha=0.3, label="Training Reward", color="gray")
+        if len(episode_rewards) > 20:
+            sm = np.convolve(episode_rewards, np.ones(20) / 20, mode="valid")
+            plt.plot(training_episodes[19:], sm, label="Training (Moving Avg)")
+        plt.plot(eval_episodes, rewards, "ro-", label="Eval Reward")
+        plt.plot(eval_episodes, avg_rewards, "go-", label="Eval Moving Avg")
+        plt.axhline(y=target_reward, color="r", linestyle="--", label="Target Reward")
+        plt.xlabel("Episode")
+        plt.ylabel("Reward")
+        plt.title(f"Training Progress ({experiment_name})")
+        plt.legend()
+        plt.grid(alpha=0.3)
+        plt.savefig(plot_path, bbox_inches="tight")
+        plt.close()
+        logger.info(f"{exp_prefix} Training plot saved to {plot_path}")
+    except Exception as e:  # plotting is cosmetic
+        logger.warning(f"{exp_prefix} plot failed: {e}")
+    csv_path = os.path.join(artifacts_dir, f"summary_{experiment_name}.csv")
+    best_model_path = os.path.join(checkpoint_dir, f"ppo_highway_best_{experiment_name}.pth")
+    with open(csv_path, "w") as f:
+        f.write("experiment,final_reward,max_reward,steps,best_model,plot\n")
+        f.write(f"{experiment_name},{avg_rewards[-1]:.4f},{max(avg_rewards):.4f},{total_steps},"
+                f"{best_model_path},{os.path.basename(plot_path)}\n")
+    logger.info(f"{exp_prefix} Summary CSV saved to {csv_path}")
+
+
+class _EvalTracker:
+    """Eval / moving-average / checkpoint bookkeeping of routine.py:172-222."""
+
+    def __init__(self, env, agent, exp_seed, target_reward, checkpoint_dir, experiment_name,
+                 metrics_history, logger, exp_prefix, start_time):
+        self.env, self.agent, self.exp_seed = env, agent, exp_seed
+        self.target_reward = target_reward
+        self.checkpoint_dir, self.name = checkpoint_dir, experiment_name
+        self.mh, self.logger, self.prefix, self.t0 = metrics_history, logger, exp_prefix, start_time
+        self.rewards, self.avg_rewards, self.eval_episodes = [], [], [0]
+        self.best = -float("inf")
+        self.solved = False
+
+    def initial(self):
+        r = evaluate(self.env, self.agent, num_episodes=5, exp_seed=self.exp_seed)
+        self.rewards.append(r)
+        self.avg_rewards.append(r)
+        self.mh["eval_rewards"].append(r)
+        self.mh["avg_eval_rewards"].append(r)
+        self.mh["eval_episode_numbers"].append(0)
+        self.mh["timestamps"].append(0)
+        self.logger.info(f"{self.prefix} initial_eval reward={r:.2f}")
+
+    def on_episode(self, episode_num):
+        self.logger.info(f"{self.prefix} Evaluating at episode {episode_num}...")
+        r = evaluate(self.env, self.agent, num_episodes=5, exp_seed=self.exp_seed)
+        self.rewards.append(r)
+        self.eval_episodes.append(episode_num)
+        elapsed = time.time() - self.t0
+        avg = float(np.mean(self.rewards[-10:])) if len(self.rewards) >= 10 else float(np.mean(self.rewards))
+        self.avg_rewards.append(avg)
+        self.mh["eval_rewards"].append(r)
+        self.mh["avg_eval_rewards"].append(avg)
+        self.mh["eval_episode_numbers"].append(episode_num)
+        self.mh["timestamps"].append(elapsed)
+        self.logger.info("%s eval episode=%d reward=%.2f avg_reward=%.2f time=%.2fs", self.prefix,
+                         episode_num, r, avg, elapsed)
+        if avg >= self.target_reward and not self.solved and len(self.rewards) >= 10:
+            self.logger.info(f"{self.prefix} Environment solved in {episode_num} episodes! avg reward={avg:.2f}")
+            self.agent.save(os.path.join(self.checkpoint_dir, f"ppo_highway_solved_{self.name}.pth"))
+            self.solved = True
+        if avg > self.best:
+            self.best = avg
+            self.agent.save(os.path.join(self.checkpoint_dir, f"ppo_highway_best_{self.name}.pth"))
+            self.logger.info(f"{self.prefix} New best model saved, avg reward={self.best:.2f}")
+
+
+# ---------------------------------------------------------------------------------- training
+def train_with_experiment_name(env, agent, max_episodes=500, target_reward=0.0, log_interval=20,
+                               eval_interval=50, steps_per_update=2048, experiment_name="",
+                               exp_seed: int = 0, logger=None):
+    if logger is None:
+        logger = setup_experiment_logger(experiment_name)
+    exp_prefix = f"[{experiment_name}]" if experiment_name else ""
+    logger.info(f"{exp_prefix} Starting training for experiment: {experiment_name}")
+    metrics_history = {
+        "experiment_name": experiment_name,
+        "episode_rewards": [],
+        "eval_rewards": [],
+        "avg_eval_rewards": [],
+        "policy_updates": [],
+        "episode_numbers": [],
+        "eval_episode_numbers": [],
+        "timestamps": [],
+    }
+    start_time = time.time()
+    artifacts_dir = ensure_artifacts_dir()
+    checkpoint_dir = os.path.join(artifacts_dir, "checkpoints")
+    os.makedirs(checkpoint_dir, exist_ok=True)
+    tracker = _EvalTracker(env, agent, exp_seed, target_reward, checkpoint_dir, experiment_name,
+                           metrics_history, logger, exp_prefix, start_time)
+    logger.info(f"{exp_prefix} Performing initial evaluation...")
+    tracker.initial()
+    loop = _train_vector if _is_vector(env) else _train_single
+    episode_rewards, training_episodes, total_steps = loop(
+        env, agent, max_episodes, log_interval, eval_interval, steps_per_update, exp_seed, logger,
+        exp_prefix, metrics_history, tracker, start_time)
+    _save_artifacts(artifacts_dir, checkpoint_dir, experiment_name, metrics_history,
+                    training_episodes, episode_rewards, tracker.eval_episodes, tracker.rewards,
+                    tracker.avg_rewards, target_reward, total_steps, logger, exp_prefix)
+    return tracker.rewards, tracker.avg_rewards, metrics_history
+
+
+def _log_episode(logger, prefix, episode_num, ep_reward, episode_rewards, log_interval,
+                 total_steps, start_time):
+    if episode_num % log_interval == 0:
+        logger.info("%s episode=%d reward=%.2f avg_reward=%.2f steps=%d time=%.2fs", prefix,
+                    episode_num, ep_reward, np.mean(episode_rewards[-log_interval:]), total_steps,
+                    time.time() - start_time)
+
+
+def _train_single(env, agent, max_episodes, log_interval, eval_interval, steps_per_update,
+                  exp_seed, logger, prefix, mh, tracker, start_time):
+    """The reference loop (routine.py:121-243) on the one-env facade."""
+    episode_rewards, training_episodes = [], []
+    total_steps = episode_num = 0
+    done, flat_state = True, None
+    while episode_num < max_episodes:
+        steps_collected = 0
+        t_update = time.time()
+        while steps_collected < steps_per_update and episode_num < max_episodes:
+            episode_num += 1
+            state, _ = env.reset(seed=exp_seed + episode_num)
+            flat_state = state.reshape(-1)
+            ep_reward, done = 0.0, False
+            while not done and steps_collected < steps_per_update:
+                action, pre_tanh, log_prob, value = agent.select_action(flat_state)
+                nxt, reward, terminated, truncated, _ = env.step(action)
+                done = terminated or truncated
+                flat_next = nxt.reshape(-1)
+                agent.memory.store(flat_state, action, pre_tanh, reward, flat_next, log_prob, done, value)
+                flat_state = flat_next
+                ep_reward += reward
+                steps_collected += 1
+                total_steps += 1
+            episode_rewards.append(ep_reward)
+            training_episodes.append(episode_num)
+            mh["episode_rewards"].append(ep_reward)
+            mh["episode_numbers"].append(episode_num)
+            _log_episode(logger, prefix, episode_num, ep_reward, episode_rewards, log_interval,
+                         total_steps, start_time)
+            if episode_num % eval_interval == 0:
+                tracker.on_episode(episode_num)
+        final_value = 0.0
+        if not done:
+            with torch.no_grad():
+                _, _, v = agent.actor_critic.forward(flat_state)
+                final_value = float(v.cpu().item())
+        upd = agent.update(last_value=final_value)
+        mh["policy_updates"].append({"episode": episode_num, "steps": steps_collected,
+                                     "time": time.time() - t_update, **upd})
+    return episode_rewards, training_episodes, total_steps
+
+
+def _train_vector(env, agent, max_episodes, log_interval, eval_interval, steps_per_update,
+                  exp_seed, logger, prefix, mh, tracker, start_time):
+    """E lockstep envs, device rollout of T steps, batched PPO update."""
+    from ppo.agent import RolloutBuffer
+
+    base = env.unwrapped
+    E = base.num_envs
+    sd = _flat_dim(env)
+    T = max(1, math.ceil(steps_per_update / E))
+    buf = RolloutBuffer(T, E, sd, 2, base.device)
+    base.set_seed_schedule(exp_seed)
+    obs, _ = env.reset()
+    buf.states[0].copy_(obs.reshape(E, sd))
+    episode_rewards, training_episodes = [], []
+    total_steps = episode_num = 0
+    while episode_num < max_episodes:
+        t_update = time.time()
+        for t in range(T):
+            a, z, lp, v = agent.select_action(buf.states[t])
+            buf.actions[t].copy_(a)
+            buf.pre_tanh[t].copy_(z)
+            buf.log_probs[t].copy_(lp)
+            buf.values[t].copy_(v)
+            base.step_into(buf.actions[t], buf.states[t + 1].view(E, *base.obs_buf.shape[1:]),
+                           buf.rewards[t], buf.terminated[t], buf.truncated[t],
+                           buf.ep_return[t], buf.ep_length[t])
+            torch.bitwise_or(buf.terminated[t], buf.truncated[t], out=buf.dones[t])
+        total_steps += T * E
+        with torch.no_grad():
+            _, _, last_v = agent.actor_critic.forward(buf.states[T])
+        upd = agent.update_rollout(buf, last_v.squeeze(-1))
+        # episode bookkeeping, in (step, env) order
+        dones = buf.dones.cpu().numpy().astype(bool)
+        rets = buf.ep_return.cpu().numpy()
+        for t, e in zip(*np.nonzero(dones)):
+            if episode_num >= max_episodes:
+                break
+            episode_num += 1
+            r = float(rets[t, e])
+            episode_rewards.append(r)
+            training_episodes.append(episode_num)
+            mh["episode_rewards"].append(r)
+            mh["episode_numbers"].append(episode_num)
+            _log_episode(logger, prefix, episode_num, r, episode_rewards, log_interval,
+                         total_steps, start_time)
+            if episode_num % eval_interval == 0:
+                tracker.on_episode(episode_num)
+        mh["policy_updates"].append({"episode": episode_num, "steps": T * E,
+                                     "time": time.time() - t_update, **upd})
+        buf.states[0].copy_(buf.states[T])
+    return episode_rewards, training_episodes, total_steps

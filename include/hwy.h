@@ -70,7 +70,13 @@ enum hwy_feature {
 enum hwy_order { HWY_ORDER_SORTED = 0, HWY_ORDER_SHUFFLED = 1 };
 
 /* Observation wrapper fused into the step (experiments/wrappers.py:91-104). */
-enum hwy_pe_kind { HWY_PE_NONE = 0, HWY_PE_RANK = 1, HWY_PE_DIST = 2, HWY_PE_ROPE = 3 };
+enum hwy_pe_kind {
+  HWY_PE_NONE = 0,
+  HWY_PE_RANK = 1,  /* RankEmbedWrapper */
+  HWY_PE_DIST = 2,  /* DistanceEmbedWrapper(use_euclidean=True) */
+  HWY_PE_ROPE = 3,  /* RotaryEmbedWrapper */
+  HWY_PE_DIST1 = 4  /* DistanceEmbedWrapper(use_euclidean=False): |x_i - x_ego| */
+};
 
 /* Mirrors HIGHWAY_CONFIG (config/base_config.py:5-39) after make_env's deep merge and
  * order resolution (experiments/wrappers.py:33-57). */
@@ -143,6 +149,8 @@ enum hwy_env_word {
 #define HWY_FLAG_PRESENT 4u
 
 int hwy_abi_version(void);
+/* sizeof(hwy_config) as compiled into the library (binding layout check). */
+int hwy_config_size(void);
 const char* hwy_last_error(void);
 
 /* Validates cfg and allocates the device state for cfg->num_envs envs on `device`. */

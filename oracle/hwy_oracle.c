@@ -480,7 +480,7 @@ static int is_relative_feature(int fid) {
  * rank_embed.py).  dist_override: RotaryEmbedWrapper._apply_rope(obs, dist_norm) entry. */
 static void apply_pe(const float* in, float* out, int N, int F, int kind, int d, int ego_idx,
                      float max_dist, const float* table, const float* dist_override) {
-  int Fo = F + ((kind == HWY_PE_RANK || kind == HWY_PE_DIST) ? d : 0);
+  int Fo = F + ((kind == HWY_PE_RANK || kind == HWY_PE_DIST || kind == HWY_PE_DIST1) ? d : 0);
   for (int i = 0; i < N; ++i) {
     const float* row = in + (size_t)i * F;
     float* o = out + (size_t)i * Fo;
@@ -495,10 +495,14 @@ static void apply_pe(const float* in, float* out, int N, int F, int kind, int d,
       nd = dist_override[i];
     } else {
       const float* eg = in + (size_t)ego_idx * F;
-      float rx = row[0] - eg[0], ry = row[1] - eg[1];
-      nd = hm_clipf(sqrtf(rx * rx + ry * ry) / max_dist, 0.0f, 1.0f);
+      if (kind == HWY_PE_DIST1) { /* dist_embed.py:84-86: |obs[:, :1] - ego[:1]| */
+        nd = hm_clipf(hm_absf(row[0] - eg[0]) / max_dist, 0.0f, 1.0f);
+      } else { /* np.linalg.norm(obs[:, :2] - ego[:2]) */
+        float rx = row[0] - eg[0], ry = row[1] - eg[1];
+        nd = hm_clipf(sqrtf(rx * rx + ry * ry) / max_dist, 0.0f, 1.0f);
+      }
     }
-    if (kind == HWY_PE_DIST) {
+    if (kind == HWY_PE_DIST || kind == HWY_PE_DIST1) {
       int h = d / 2;
       for (int k = 0; k < h; ++k) {
         float ang = (HM_TWO_PI_F * nd) * table[k];
@@ -703,8 +707,9 @@ static void step_road(Road* r, const float* action, float* obs, float* reward, u
 
 /* ================================================================== exported oracle ABI */
 static int obs_fout(const hwy_config* cfg) {
+  int k = cfg->pe_kind;
   return cfg->n_features +
-         ((cfg->pe_kind == HWY_PE_RANK || cfg->pe_kind == HWY_PE_DIST) ? cfg->d_embed : 0);
+         ((k == HWY_PE_RANK || k == HWY_PE_DIST || k == HWY_PE_DIST1) ? cfg->d_embed : 0);
 }
 
 int hwyo_reset(const hwy_config* cfg, uint32_t* state, const uint64_t* seeds, const uint8_t* mask,
@@ -751,7 +756,7 @@ int hwyo_observe(const hwy_config* cfg, uint32_t* state, float* obs, const float
 
 int hwyo_obs_pe(const float* obs_in, float* obs_out, int E, int N, int F, int kind, int d,
                 int ego_idx, float max_dist, const float* table, const float* dist_override) {
-  int Fo = F + ((kind == HWY_PE_RANK || kind == HWY_PE_DIST) ? d : 0);
+  int Fo = F + ((kind == HWY_PE_RANK || kind == HWY_PE_DIST || kind == HWY_PE_DIST1) ? d : 0);
   for (int e = 0; e < E; ++e)
     apply_pe(obs_in + (size_t)e * N * F, obs_out + (size_t)e * N * Fo, N, F, kind, d, ego_idx,
              max_dist, table, dist_override ? dist_override + (size_t)e * N : NULL);
@@ -805,6 +810,8 @@ int hwyo_math(int op, const float* in, const float* in2, float* out, int n) {
   }
   return 0;
 }
+
+int hwyo_config_size(void) { return (int)sizeof(hwy_config); }
 
 /* Philox known-answer check helper */
 void hwyo_philox(const uint32_t* ctr, const uint32_t* key, uint32_t* out) {

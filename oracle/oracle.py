@@ -127,7 +127,7 @@ def obs_pe(obs: np.ndarray, kind: int, d: int, ego_idx: int, max_dist: float,
     if squeeze:
         obs = obs[None]
     E, N, F = obs.shape
-    Fo = F + (d if kind in (1, 2) else 0)
+    Fo = F + (d if kind in (1, 2, 4) else 0)
     out = np.zeros((E, N, Fo), np.float32)
     t = None if table is None else np.ascontiguousarray(table, np.float32)
     dov = None if dist_override is None else np.ascontiguousarray(dist_override, np.float32).reshape(E, N)

@@ -1,0 +1,137 @@
+"""Known-answer and invariant tests of the oracle env (highway-env 1.10.1 restatement).
+
+highway-env is absent offline, so its dynamics are PARITY UNPINNED against upstream; these
+tests pin the restatement to closed forms and to the invariants upstream guarantees."""
+
+import numpy as np
+
+from hwy import _abi
+from oracle.oracle import OracleEnv
+from parity_util import make_cfg
+
+F32 = np.float32
+
+
+def _fresh(E=8, **kw):
+    cfg = make_cfg(E=E, autoreset=False, **kw)
+    env = OracleEnv(cfg)
+    obs = env.reset()
+    return cfg, env, obs
+
+
+def test_reset_traffic_layout():
+    """HighwayEnv._create_vehicles: ego first at 3*offset + offset*U(0.9,1.1); traffic placed
+    successively ahead; lanes 0..3 on y = 4*lane; speeds U(21, 24); ego 25 m/s."""
+    cfg, env, obs = _fresh()
+    V = cfg.vehicles_count + 1
+    x = env.ffield(_abi.F_X)[:, :V]
+    y = env.ffield(_abi.F_Y)[:, :V]
+    spd = env.ffield(_abi.F_SPEED)[:, :V]
+    assert np.all(np.diff(x, axis=1) > 0), "each car is placed ahead of all previous ones"
+    assert np.all(spd[:, 0] == 25.0)
+    assert np.all((spd[:, 1:] >= 21.0) & (spd[:, 1:] < 24.0))
+    assert set(np.unique(y)) <= {0.0, 4.0, 8.0, 12.0}
+    off0 = 2 * (12 + 25) * np.exp(-0.5)
+    assert np.all((x[:, 0] > 3 * off0 + 0.89 * off0) & (x[:, 0] < 3 * off0 + 1.11 * off0))
+    delta = env.ffield(_abi.F_DELTA)[:, 1:V]
+    assert np.all((delta >= 3.5) & (delta < 4.5))
+    timer = env.ffield(_abi.F_TIMER)[:, 1:V]
+    want = ((x[:, 1:] + y[:, 1:]) * F32(np.pi)) % 1.0
+    np.testing.assert_allclose(timer, want, atol=2e-4)
+
+
+def test_reset_observation_is_normalised_relative_sorted():
+    cfg, env, obs = _fresh()
+    # ego row: absolute x clipped to 1, y = lane/25, vx = 25/30
+    assert np.all(obs[:, 0, 0] == 1.0)
+    np.testing.assert_allclose(obs[:, 0, 2], 25.0 / 30.0, rtol=1e-6)
+    # other rows relative and sorted by |dx|
+    dx = obs[:, 1:, 0]
+    present = np.any(obs[:, 1:] != 0, axis=2)
+    for e in range(obs.shape[0]):
+        d = np.abs(dx[e][present[e]])
+        assert np.all(np.diff(d) >= 0)
+
+
+def test_idm_free_road_acceleration_closed_form():
+    """A lone IDM car: a = 3 * (1 - (v / v0)^delta) (IDMVehicle.acceleration, no front car)."""
+    cfg = make_cfg(E=1, autoreset=False, vehicles_count=1, lanes_count=1)
+    env = OracleEnv(cfg)
+    env.reset()
+    st = env.state
+    st[_abi.F_X, 0, 0] = np.float32(0.0).view(np.uint32)  # ego far behind, different world
+    st[_abi.F_X, 0, 1] = np.float32(500.0).view(np.uint32)
+    v0, v, delta = 28.0, 20.0, 4.0
+    st[_abi.F_SPEED, 0, 1] = np.float32(v).view(np.uint32)
+    st[_abi.F_TSPEED, 0, 1] = np.float32(v0).view(np.uint32)
+    st[_abi.F_DELTA, 0, 1] = np.float32(delta).view(np.uint32)
+    env.step(np.zeros((1, 2), np.float32))
+    spd = env.ffield(_abi.F_SPEED)[0, 1]
+    # integrate the 15 frames in double precision
+    vv = v
+    for _ in range(15):
+        vv += 3.0 * (1 - (max(vv, 0) / v0) ** delta) / 15.0
+    assert abs(spd - vv) < 1e-4
+
+
+def test_ego_crash_terminates_and_rewards_collision():
+    """Driving into the car ahead: crashed -> terminated, reward uses collision_reward."""
+    cfg = make_cfg(E=1, autoreset=False, vehicles_count=1, lanes_count=1)
+    env = OracleEnv(cfg)
+    env.reset()
+    st = env.state
+    st[_abi.F_X, 0, 0] = np.float32(100.0).view(np.uint32)
+    st[_abi.F_X, 0, 1] = np.float32(112.0).view(np.uint32)
+    st[_abi.F_SPEED, 0, 1] = np.float32(0.0).view(np.uint32)
+    st[_abi.F_TSPEED, 0, 1] = np.float32(0.0).view(np.uint32)
+    _, r, te, tr, _, _ = env.step(np.array([[1.0, 0.0]], np.float32))
+    assert te[0] and not tr[0]
+    # crashed: r = (-1 + 0 + 0.4*clip(lmap(v))) -> lmap over [-1, 0.5]
+    spd = env.ffield(_abi.F_SPEED)[0, 0]
+    hs = np.clip((spd - 20) / 10, 0, 1)
+    want = (-1 + 0.4 * hs + 1) / 1.5
+    assert abs(r[0] - want) < 1e-5
+
+
+def test_truncation_at_horizon_and_autoreset_schedule():
+    cfg = make_cfg(E=3, autoreset=True, max_episode_steps=4, seed_base=100)
+    env = OracleEnv(cfg)
+    env.reset()
+    seeds0 = env.field(_abi.F_ENV)[:, _abi.E_SEED_LO].copy()
+    assert list(seeds0) == [101, 102, 103]  # exp_seed + 1 + e
+    episodes = np.zeros(3, int)
+    for t in range(4):
+        _, _, te, tr, ret, ln = env.step(np.zeros((3, 2), np.float32))
+        assert np.all(ln[tr & ~te] == 4)  # truncation exactly at the horizon
+        assert np.all((ln > 0) == (te | tr))
+        episodes += te | tr
+    assert np.all(episodes >= 1)  # the horizon ends every episode by step 4
+    seeds1 = env.field(_abi.F_ENV)[:, _abi.E_SEED_LO].astype(int)
+    assert list(seeds1) == [101 + e + 3 * k for e, k in enumerate(episodes)]  # + seed_stride * k
+
+
+def test_shuffled_order_is_a_permutation_of_sorted_rows():
+    cfg_s = make_cfg(E=6, order="sorted", autoreset=False)
+    cfg_u = make_cfg(E=6, order="shuffled", autoreset=False)
+    a, b = OracleEnv(cfg_s), OracleEnv(cfg_u)
+    oa, ob = a.reset(), b.reset()
+    for e in range(6):
+        assert np.array_equal(oa[e, 0], ob[e, 0])
+        ra = sorted(map(tuple, oa[e, 1:]))
+        rb = sorted(map(tuple, ob[e, 1:]))
+        assert ra == rb
+
+
+def test_lane_changes_and_collisions_occur_in_traffic():
+    cfg = make_cfg(E=16, autoreset=True)
+    env = OracleEnv(cfg)
+    env.reset()
+    rng = np.random.default_rng(0)
+    changed = crashes = 0
+    V = cfg.vehicles_count + 1
+    for _ in range(20):
+        a = np.tanh(rng.normal(size=(16, 2)) * [0.5, 0.05]).astype(np.float32)
+        _, _, te, _, _, _ = env.step(a)
+        crashes += te.sum()
+        changed += (env.field(_abi.F_LANE)[:, 1:V] != env.field(_abi.F_TLANE)[:, 1:V]).sum()
+    assert changed > 0 and crashes > 0
