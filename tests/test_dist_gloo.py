@@ -1,0 +1,92 @@
+"""Env-sharded data parallelism on CPU with gloo, world size 2.
+
+Each rank owns its own slice of samples; per optimizer step the flat gradient bucket is
+all-reduced (mean), and advantage statistics are reduced once per update.  The sharded result
+must equal one process running the same update on the concatenated data with global
+minibatch i = rank0's minibatch i ++ rank1's minibatch i."""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+SD, H, EPOCHS, NMB, NLOC = 12, 16, 3, 4, 64
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _data(rank, n=NLOC):
+    g = np.random.default_rng(100 + rank)
+    return dict(
+        s=torch.as_tensor(g.normal(size=(n, SD)).astype(np.float32)),
+        z=torch.as_tensor(g.normal(size=(n, 2)).astype(np.float32) * 0.5),
+        lp=torch.as_tensor(g.normal(size=n).astype(np.float32) - 2.0),
+        a=torch.as_tensor(g.normal(size=n).astype(np.float32)),
+        r=torch.as_tensor(g.normal(size=n).astype(np.float32)),
+        perm=torch.as_tensor(g.permutation(n)),
+    )
+
+
+def _make_agent(group=None):
+    import sys
+
+    from ppo.agent import PPOAgent
+
+    torch.manual_seed(7)
+    return PPOAgent(SD, 2, lr=1e-3, epochs=EPOCHS, batch_size=16, hidden_dim=H,
+                    device=torch.device("cpu"), num_minibatches=NMB, use_graphs=False,
+                    process_group=group)
+
+
+def _worker(rank, world, port, out_dir):
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.join(os.path.dirname(here), "highway-rope-ppo_amd"), here]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    if rank == 1:
+        torch.manual_seed(999)  # different local init: the broadcast must make weights equal
+    agent = _make_agent(torch.distributed.group.WORLD)
+    d = _data(rank)
+    adv_n = agent.normalize_advantages(d["a"])
+    mb = NLOC // NMB
+    batches = [d["perm"][i * mb:(i + 1) * mb] for i in range(NMB)]
+    agent._run_epochs(d["s"], d["z"], d["lp"], adv_n, d["r"], batches)
+    torch.save({"state": agent.actor_critic.state_dict(), "adv": adv_n},
+               os.path.join(out_dir, f"rank{rank}.pt"))
+    torch.distributed.destroy_process_group()
+
+
+def test_sharded_update_equals_single_process(tmp_path):
+    port = _free_port()
+    mp.start_processes(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    # replicas stay identical
+    for k in r0["state"]:
+        torch.testing.assert_close(r0["state"][k], r1["state"][k], rtol=0, atol=0)
+    # single process on the concatenated data
+    d0, d1 = _data(0), _data(1)
+    cat = {k: torch.cat([d0[k], d1[k]]) for k in ("s", "z", "lp", "a", "r")}
+    a = cat["a"]
+    adv_n = (a - a.mean()) / (a.std() + 1e-8)
+    torch.testing.assert_close(torch.cat([r0["adv"], r1["adv"]]), adv_n, rtol=1e-5, atol=1e-6)
+    agent = _make_agent(None)
+    mb = NLOC // NMB
+    batches = [torch.cat([d0["perm"][i * mb:(i + 1) * mb], d1["perm"][i * mb:(i + 1) * mb] + NLOC])
+               for i in range(NMB)]
+    agent._run_epochs(cat["s"], cat["z"], cat["lp"], adv_n, cat["r"], batches)
+    for k, v in agent.actor_critic.state_dict().items():
+        torch.testing.assert_close(r0["state"][k], v, rtol=2e-5, atol=2e-6, msg=k)
