@@ -692,7 +692,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt) {
 }
 
 // ------------------------------------------------------------------------- kernels
-__global__ void __launch_bounds__(256) hwy_step_kernel(StepParams P) {
+__global__ void __launch_bounds__(256, 4) hwy_step_kernel(StepParams P) {
   __shared__ int lds_vor[ENVS_PER_BLOCK][WAVE];
   __shared__ int lds_inv[ENVS_PER_BLOCK][WAVE];
   const hwy_config& C = P.cfg;

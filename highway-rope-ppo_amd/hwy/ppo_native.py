@@ -1,0 +1,225 @@
+"""Driver of the fused PPO minibatch step in libhwy.so (include/hwy_ppo.h).
+
+``FusedPPO`` owns the flat parameter / gradient / Adam buffers of an ActorCritic (the module's
+parameters are re-pointed into the flat buffer, so state_dict(), checkpoints and the torch
+forward used for acting see the same storage) and runs one update's minibatch steps:
+
+  * single GPU: one HIP graph per epoch (minibatch i uses perm[i*mb:(i+1)*mb] of a static
+    permutation buffer; the same partition is replayed for every epoch, ppo/agent.py:205);
+  * with a process group: per minibatch, graph(forward+backward) -> RCCL all-reduce of the flat
+    gradient (mean) -> graph(clip + Adam).
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional
+
+import torch
+
+from .native import check, lib, stream_ptr
+
+_PARAM_ORDER = ("shared.0.weight", "shared.0.bias", "shared.2.weight", "shared.2.bias",
+                "actor_mean.0.weight", "actor_mean.0.bias", "actor_mean.2.weight",
+                "actor_mean.2.bias", "log_std", "critic.0.weight", "critic.0.bias",
+                "critic.2.weight", "critic.2.bias")
+
+
+class PpoDims(ctypes.Structure):
+    _fields_ = [("B", ctypes.c_int32), ("S", ctypes.c_int32), ("H", ctypes.c_int32),
+                ("A", ctypes.c_int32)]
+
+
+class PpoArgs(ctypes.Structure):
+    _fields_ = [
+        ("dims", PpoDims),
+        ("states", ctypes.c_void_p), ("pre_tanh", ctypes.c_void_p), ("old_logp", ctypes.c_void_p),
+        ("adv", ctypes.c_void_p), ("ret", ctypes.c_void_p), ("idx", ctypes.c_void_p),
+        ("params", ctypes.c_void_p), ("grads", ctypes.c_void_p), ("adam_m", ctypes.c_void_p),
+        ("adam_v", ctypes.c_void_p), ("counters", ctypes.c_void_p), ("metrics", ctypes.c_void_p),
+        ("workspace", ctypes.c_void_p),
+        ("eps_clip", ctypes.c_float), ("value_coef", ctypes.c_float),
+        ("entropy_coef", ctypes.c_float), ("max_grad_norm", ctypes.c_float),
+        ("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
+        ("adam_eps", ctypes.c_float), ("grads_modified", ctypes.c_int32),
+    ]
+
+
+def _bind(L):
+    if getattr(L, "_ppo_bound", False):
+        return L
+    L.hwy_ppo_param_layout.argtypes = [ctypes.POINTER(PpoDims), ctypes.c_void_p, ctypes.c_void_p]
+    L.hwy_ppo_param_layout.restype = ctypes.c_int
+    L.hwy_ppo_workspace_bytes.argtypes = [ctypes.POINTER(PpoDims)]
+    L.hwy_ppo_workspace_bytes.restype = ctypes.c_int64
+    L.hwy_ppo_forward_backward.argtypes = [ctypes.POINTER(PpoArgs), ctypes.c_void_p]
+    L.hwy_ppo_forward_backward.restype = ctypes.c_int
+    L.hwy_ppo_optimizer.argtypes = [ctypes.POINTER(PpoArgs), ctypes.c_void_p]
+    L.hwy_ppo_optimizer.restype = ctypes.c_int
+    L._ppo_bound = True
+    return L
+
+
+def param_layout(S: int, H: int, B: int = 64):
+    L = _bind(lib())
+    d = PpoDims(B, S, H, 2)
+    offs = (ctypes.c_int64 * 13)()
+    n = ctypes.c_int64()
+    if L.hwy_ppo_param_layout(ctypes.byref(d), offs, ctypes.byref(n)) != 0:
+        raise ValueError(f"fused PPO supports action_dim 2 and hidden_dim a multiple of 64 "
+                         f"(<= 512); got S={S} H={H}")
+    return list(offs), int(n.value)
+
+
+class FusedPPO:
+    def __init__(self, agent, mb: int, nmb: int, group=None, use_graphs: bool = True):
+        ac = agent.actor_critic
+        self.agent = agent
+        dev = agent.device
+        named = dict(ac.named_parameters())
+        if set(named.keys()) != set(_PARAM_ORDER):
+            raise ValueError("unexpected ActorCritic parameter layout for the fused step")
+        S = named["shared.0.weight"].shape[1]
+        H = named["shared.0.weight"].shape[0]
+        if named["log_std"].numel() != 2:
+            raise ValueError("fused PPO step needs action_dim == 2")
+        self.S, self.H, self.mb, self.nmb = S, H, mb, nmb
+        offs, numel = param_layout(S, H, mb)
+        L = _bind(lib())
+        self.L = L
+        self.dims = PpoDims(mb, S, H, 2)
+        ws = L.hwy_ppo_workspace_bytes(ctypes.byref(self.dims))
+        if ws < 0:
+            raise ValueError("unsupported fused PPO dims")
+        self.flat = torch.empty(numel, device=dev, dtype=torch.float32)
+        self.grads = torch.zeros(numel, device=dev, dtype=torch.float32)
+        self.m = torch.zeros(numel, device=dev, dtype=torch.float32)
+        self.v = torch.zeros(numel, device=dev, dtype=torch.float32)
+        self.params: List[torch.nn.Parameter] = []
+        with torch.no_grad():
+            for name, off in zip(_PARAM_ORDER, offs):
+                p = named[name]
+                n = p.numel()
+                self.flat[off:off + n].copy_(p.detach().reshape(-1))
+                p.data = self.flat[off:off + n].view_as(p)
+                p.grad = self.grads[off:off + n].view_as(p)
+                self.params.append(p)
+        self.offs = offs
+        self.workspace = torch.empty(int(ws), device=dev, dtype=torch.uint8)
+        self.counters = torch.zeros(2, device=dev, dtype=torch.int32)
+        self.metrics = torch.zeros(max(1, agent.epochs * nmb), 6, device=dev)
+        self.group = group
+        self.world = 1 if group is None else torch.distributed.get_world_size(group)
+        self.use_graphs = use_graphs
+        self._import_torch_state()
+        self._graphs = None
+        self._bound_key = None
+
+    # -------------------------------------------------------------- optimizer state <-> torch
+    def _import_torch_state(self):
+        opt = self.agent.optimizer
+        st0 = opt.state.get(self.params[0])
+        if not st0:
+            return
+        with torch.no_grad():
+            for p, off in zip(self.params, self.offs):
+                st = opt.state[p]
+                n = p.numel()
+                self.m[off:off + n].copy_(st["exp_avg"].reshape(-1))
+                self.v[off:off + n].copy_(st["exp_avg_sq"].reshape(-1))
+            self.counters[0] = int(float(st0["step"]))
+
+    def export_torch_state(self):
+        """Write the fused Adam state into agent.optimizer (torch.optim.Adam layout)."""
+        opt = self.agent.optimizer
+        t = int(self.counters[0].item())
+        if t == 0:
+            return
+        for p, off in zip(self.params, self.offs):
+            n = p.numel()
+            opt.state[p] = {
+                "step": torch.tensor(float(t), device=p.device if opt.defaults.get("capturable") else "cpu"),
+                "exp_avg": self.m[off:off + n].view_as(p).clone(),
+                "exp_avg_sq": self.v[off:off + n].view_as(p).clone(),
+            }
+
+    # -------------------------------------------------------------- steps
+    def _args(self, states, pre_tanh, old_lp, adv, ret, idx_ptr: int) -> PpoArgs:
+        ag = self.agent
+        a = PpoArgs()
+        a.dims = self.dims
+        a.states, a.pre_tanh, a.old_logp = states.data_ptr(), pre_tanh.data_ptr(), old_lp.data_ptr()
+        a.adv, a.ret, a.idx = adv.data_ptr(), ret.data_ptr(), idx_ptr
+        a.params, a.grads = self.flat.data_ptr(), self.grads.data_ptr()
+        a.adam_m, a.adam_v = self.m.data_ptr(), self.v.data_ptr()
+        a.counters, a.metrics = self.counters.data_ptr(), self.metrics.data_ptr()
+        a.workspace = self.workspace.data_ptr()
+        a.eps_clip, a.value_coef, a.entropy_coef = ag.eps_clip, ag.value_coef, ag.entropy_coef
+        a.max_grad_norm = ag.max_grad_norm
+        g = ag.optimizer.param_groups[0]
+        a.lr, (a.beta1, a.beta2), a.adam_eps = g["lr"], g["betas"], g["eps"]
+        a.grads_modified = 1 if self.group is not None else 0
+        return a
+
+    def _fwd_bwd(self, a):
+        check(self.L.hwy_ppo_forward_backward(ctypes.byref(a), stream_ptr()), "hwy_ppo_forward_backward")
+
+    def _opt(self, a):
+        check(self.L.hwy_ppo_optimizer(ctypes.byref(a), stream_ptr()), "hwy_ppo_optimizer")
+
+    def _allreduce(self):
+        torch.distributed.all_reduce(self.grads, group=self.group)
+        self.grads.div_(self.world)
+
+    def run(self, states, pre_tanh, old_lp, adv, ret, perm: torch.Tensor) -> torch.Tensor:
+        """All epochs of one update; returns the [epochs*nmb, 6] metrics rows (device)."""
+        mb, nmb, epochs = self.mb, self.nmb, self.agent.epochs
+        key = (states.data_ptr(), pre_tanh.data_ptr(), old_lp.data_ptr(), adv.data_ptr(),
+               ret.data_ptr(), perm.data_ptr())
+        args = [self._args(states, pre_tanh, old_lp, adv, ret, perm.data_ptr() + i * mb * 8)
+                for i in range(nmb)]
+        self.counters[1].zero_()
+        if not self.use_graphs:
+            for _ in range(epochs):
+                for a in args:
+                    self._fwd_bwd(a)
+                    if self.group is not None:
+                        self._allreduce()
+                    self._opt(a)
+            return self.metrics
+        if self._graphs is None or self._bound_key != key:
+            self._capture(args)
+            self._bound_key = key
+        for _ in range(epochs):
+            if self.group is None:
+                self._graphs[0].replay()
+            else:
+                for gf, go in self._graphs:
+                    gf.replay()
+                    self._allreduce()
+                    go.replay()
+        return self.metrics
+
+    def _capture(self, args):
+        self._keep_args = args
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        graphs = []
+        with torch.cuda.stream(s):
+            if self.group is None:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    for a in args:
+                        self._fwd_bwd(a)
+                        self._opt(a)
+                graphs.append(g)
+            else:
+                for a in args:
+                    gf, go = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(gf, stream=s):
+                        self._fwd_bwd(a)
+                    with torch.cuda.graph(go, stream=s):
+                        self._opt(a)
+                    graphs.append((gf, go))
+        torch.cuda.current_stream().wait_stream(s)
+        self._graphs = graphs

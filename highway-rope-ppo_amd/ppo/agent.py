@@ -309,8 +309,14 @@ class PPOAgent:
                  logger: Optional[logging.Logger] = None,
                  device: torch.device = torch.device("cpu"),
                  num_minibatches: Optional[int] = None, use_graphs: bool = True,
-                 process_group=None, seed: Optional[int] = None):
+                 process_group=None, seed: Optional[int] = None, backend: str = "auto"):
         self.device = torch.device(device)
+        if backend not in ("auto", "hip", "torch"):
+            raise ValueError(f"backend must be auto|hip|torch, got {backend!r}")
+        # "hip": update_rollout runs the fused HIP minibatch step (hwy/ppo_native.py);
+        # "torch": autograd + torch.optim.Adam (the reference arithmetic, also used by update())
+        self.backend = backend
+        self._fused = None
         self.actor_critic = ActorCritic(state_dim, action_dim, hidden_dim, device=self.device)
         self._dist = process_group
         if process_group is not None:  # identical initial weights on every rank
@@ -449,14 +455,50 @@ class PPOAgent:
         if perm is None:
             perm = torch.randperm(n, device=self.device, generator=self.generator)
         mb = n // nmb
-        batches = [perm[i * mb:(i + 1) * mb] for i in range(nmb)]  # one partition, all epochs
-        rows = self._run_epochs(states, pre_tanh, old_lp, adv, ret, batches)
+        if self._fused_ok(mb):
+            F = self._fused_for(mb, nmb, n)
+            F_adv, F_ret, F_perm = self._static_bufs
+            F_adv.copy_(adv)
+            F_ret.copy_(ret)
+            F_perm.copy_(perm)
+            rows = F.run(states, pre_tanh, old_lp, F_adv, F_ret, F_perm)
+        else:
+            batches = [perm[i * mb:(i + 1) * mb] for i in range(nmb)]  # one partition, all epochs
+            rows = self._run_epochs(states, pre_tanh, old_lp, adv, ret, batches)
         if not return_metrics:
             return rows
         return self._finish_metrics(rows.cpu().numpy(), [mb] * nmb, buf.values.reshape(n), ret)
 
+    # ------------------------------------------------------------------ fused HIP step
+    def _fused_ok(self, mb: int) -> bool:
+        if self.backend == "torch" or self.device.type != "cuda":
+            return False
+        sd = self.actor_critic.shared[0].weight
+        H = sd.shape[0]
+        ok = self.actor_critic.log_std.numel() == 2 and H % 64 == 0 and 64 <= H <= 512
+        if not ok and self.backend == "hip":
+            raise ValueError("backend='hip' needs action_dim 2 and hidden_dim in {64,128,...,512}")
+        return ok
+
+    def _fused_for(self, mb: int, nmb: int, n: int):
+        from hwy.ppo_native import FusedPPO
+
+        F = self._fused
+        if F is None or F.mb != mb or F.nmb != nmb or F.metrics.shape[0] != self.epochs * nmb:
+            F = FusedPPO(self, mb, nmb, group=self._dist, use_graphs=self.use_graphs)
+            self._fused = F
+            self._learner = None
+        bufs = getattr(self, "_static_bufs", None)
+        if bufs is None or bufs[0].numel() != n:
+            dev = self.device
+            self._static_bufs = (torch.empty(n, device=dev), torch.empty(n, device=dev),
+                                 torch.empty(n, device=dev, dtype=torch.int64))
+        return F
+
     # ------------------------------------------------------------------ checkpoints
     def save(self, path: str):
+        if self._fused is not None:
+            self._fused.export_torch_state()
         torch.save({"model": self.actor_critic.state_dict(),
                     "optimizer": self.optimizer.state_dict()}, path)
         self.logger.info(f"model_saved path={path}")
@@ -466,6 +508,8 @@ class PPOAgent:
         self.actor_critic.load_state_dict(ckpt["model"])
         if load_optimizer and "optimizer" in ckpt:
             self.optimizer.load_state_dict(ckpt["optimizer"])
+            if self._fused is not None:
+                self._fused._import_torch_state()
         self._learner = None
         self.logger.info(f"model_loaded path={path}")
         return ckpt.get("config", {})

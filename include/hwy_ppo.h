@@ -1,0 +1,72 @@
+/*
+ * hwy_ppo.h -- C ABI of the fused PPO minibatch step (libhwy.so).
+ *
+ * Replaces, for the batched path, the per-minibatch body of PPOAgent.update
+ * (reference ppo/agent.py:216-252): ActorCritic.evaluate (:76-84) on the minibatch, the
+ * ratio / KL / clipped surrogate / MSE / entropy loss (:226-245), loss.backward(),
+ * clip_grad_norm_(0.5) (:249-251) and Adam.step() (:252, torch.optim.Adam defaults).
+ *
+ * Network (ppo/agent.py:23-42): shared = Lin(S,H)-ReLU-Lin(H,H)-ReLU; actor_mean =
+ * Lin(H,H)-ReLU-Lin(H,A); log_std[A]; critic = Lin(H,H)-ReLU-Lin(H,1).  Parameters live in
+ * one flat fp32 buffer in nn.Module.parameters() order:
+ *   shared.0.{weight,bias} shared.2.{weight,bias} actor_mean.0.{weight,bias}
+ *   actor_mean.2.{weight,bias} log_std critic.0.{weight,bias} critic.2.{weight,bias}
+ * (weights [out, in] row-major, as nn.Linear stores them).
+ *
+ * All math is fp32; GEMMs use v_mfma_f32_32x32x2_f32 (exact fp32 products, fp32 accumulate).
+ * Calls are asynchronous, allocate nothing and are hipGraph-capturable.
+ */
+#ifndef HWY_PPO_H_
+#define HWY_PPO_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct hwy_ppo_dims {
+  int32_t B; /* minibatch rows */
+  int32_t S; /* state_dim */
+  int32_t H; /* hidden_dim (multiple of 64) */
+  int32_t A; /* action_dim (2) */
+} hwy_ppo_dims;
+
+/* Flat-parameter offsets (floats) for dims; numel returned. */
+int hwy_ppo_param_layout(const hwy_ppo_dims* d, int64_t* offsets /*[13]*/, int64_t* numel);
+/* Workspace bytes needed by hwy_ppo_forward_backward / hwy_ppo_optimizer for dims. */
+int64_t hwy_ppo_workspace_bytes(const hwy_ppo_dims* d);
+
+typedef struct hwy_ppo_args {
+  hwy_ppo_dims dims;
+  /* rollout sources (flattened [n, ...]) and this minibatch's row indices [B] (int64) */
+  const float* states;    /* [n, S] */
+  const float* pre_tanh;  /* [n, A] */
+  const float* old_logp;  /* [n] */
+  const float* adv;       /* [n] normalised advantages */
+  const float* ret;       /* [n] returns */
+  const int64_t* idx;     /* [B] */
+  /* model / optimizer state (flat, hwy_ppo_param_layout order) */
+  float* params;
+  float* grads;
+  float* adam_m;
+  float* adam_v;
+  int32_t* counters;      /* [0] Adam step t, [1] metrics row */
+  float* metrics;         /* [rows, 6]: policy, value, entropy, loss, clip count, kl */
+  void* workspace;
+  /* hyper-parameters (PPOAgent defaults: eps_clip .2, value_coef .5, entropy_coef .005) */
+  float eps_clip, value_coef, entropy_coef, max_grad_norm;
+  float lr, beta1, beta2, adam_eps;
+  int32_t grads_modified; /* grads changed after forward_backward (e.g. all-reduced): the
+                             optimizer recomputes the gradient norm from them */
+} hwy_ppo_args;
+
+/* Forward, loss, backward: writes grads (flat) and the metrics row. */
+int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream);
+/* clip_grad_norm_(max_grad_norm) + Adam step on params (call after any gradient all-reduce). */
+int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HWY_PPO_H_ */

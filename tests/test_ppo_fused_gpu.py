@@ -1,0 +1,143 @@
+"""The fused HIP PPO minibatch step (csrc/ppo_kernels.hip) against torch autograd + torch Adam
+running the reference's per-minibatch math (ppo/agent.py:216-252), fp32 tolerance."""
+
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from hwy.ppo_native import FusedPPO
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _agents(S, H, backend_b="hip", seed=0, **kw):
+    from ppo.agent import PPOAgent
+
+    torch.manual_seed(seed)
+    a = PPOAgent(S, 2, lr=3e-4, epochs=kw.get("epochs", 2), hidden_dim=H, device=DEV,
+                 use_graphs=False, backend="torch")
+    b = PPOAgent(S, 2, lr=3e-4, epochs=kw.get("epochs", 2), hidden_dim=H, device=DEV,
+                 use_graphs=kw.get("graphs", False), backend=backend_b)
+    b.actor_critic.load_state_dict(a.actor_critic.state_dict())
+    with torch.no_grad():
+        a.actor_critic.log_std.copy_(torch.tensor([-0.4, 0.3]))
+        b.actor_critic.log_std.copy_(torch.tensor([-0.4, 0.3]))
+    return a, b
+
+
+def _data(n, S, agent, seed=1):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    s = torch.randn(n, S, device=DEV, generator=g)
+    with torch.no_grad():
+        _, z, lp, v = agent.actor_critic.act(s, generator=g)
+    lp = lp + 0.05 * torch.randn(n, device=DEV, generator=g)  # ratios != 1, some clipped
+    adv = torch.randn(n, device=DEV, generator=g)
+    ret = v + torch.randn(n, device=DEV, generator=g)
+    perm = torch.randperm(n, device=DEV, generator=g)
+    return s, z.contiguous(), lp.contiguous(), adv, ret, perm
+
+
+def _torch_grad(agent, s, z, lp, adv, ret, idx):
+    from ppo.agent import _Learner
+
+    L = _Learner(agent, s.shape[0], idx.numel(), 1, False)
+    L.bind(s, z, lp, adv, ret)
+    L.idx.copy_(idx)
+    L._fwd_bwd()
+    return L.flat_grad.clone(), L.metrics[0].clone()
+
+
+@pytest.mark.parametrize("S,H,mb", [(60, 256, 512), (60, 64, 256), (120, 512, 256), (136, 128, 128)])
+def test_fused_gradient_matches_autograd(S, H, mb):
+    a, b = _agents(S, H)
+    n = mb * 2
+    s, z, lp, adv, ret, perm = _data(n, S, a)
+    idx = perm[:mb].contiguous()
+    g_ref, m_ref = _torch_grad(a, s, z, lp, adv, ret, idx)
+    F = FusedPPO(b, mb, 2, use_graphs=False)
+    args = F._args(s, z, lp, adv, ret, idx.data_ptr())
+    F.counters.zero_()
+    F._fwd_bwd(args)
+    torch.cuda.synchronize()
+    ga = dict(a.actor_critic.named_parameters())
+    gb = dict(b.actor_critic.named_parameters())
+    for name, pa in ga.items():
+        ref = pa.grad
+        scale = max(ref.abs().max().item(), 1e-3)
+        torch.testing.assert_close(gb[name].grad, ref, rtol=1e-3, atol=2e-5 * scale, msg=name)
+    m = F.metrics[0]
+    # policy, value, entropy, loss, clip count, kl
+    torch.testing.assert_close(m, m_ref, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_fused_update_matches_torch_update(graphs):
+    S, H, n, nmb = 60, 256, 2048, 4
+    a, b = _agents(S, H, graphs=graphs, epochs=3)
+    s, z, lp, adv, ret, perm = _data(n, S, a)
+    mb = n // nmb
+    rows_a = a._run_epochs(s, z, lp, adv, ret, [perm[i * mb:(i + 1) * mb] for i in range(nmb)])
+    F = FusedPPO(b, mb, nmb, use_graphs=graphs)
+    rows_b = F.run(s, z, lp, adv.clone(), ret.clone(), perm.clone())
+    torch.cuda.synchronize()
+    steps = 3 * nmb
+    for (k, va), (_, vb) in zip(a.actor_critic.state_dict().items(), b.actor_critic.state_dict().items()):
+        # Adam normalises each element's step (~lr * sign(g) early on), so elements whose
+        # gradient is at fp32 noise level may step differently: bound the worst case by the
+        # largest possible move and require nearly all elements to agree closely.
+        d = (va - vb).abs()
+        assert d.max().item() <= 2 * 3e-4 * steps, k
+        assert (d > 2e-5).float().mean().item() < 0.05, (k, d.max().item())
+    torch.testing.assert_close(rows_b, rows_a, rtol=5e-3, atol=5e-5)
+    assert int(F.counters[0]) == steps
+
+
+def test_fused_optimizer_matches_torch_adam_on_identical_grads():
+    """clip_grad_norm_(0.5) + torch.optim.Adam vs the fused optimizer kernel, same gradients."""
+    S, H = 60, 128
+    a, b = _agents(S, H)
+    F = FusedPPO(b, 128, 1, use_graphs=False)
+    pa = dict(a.actor_critic.named_parameters())
+    pb = dict(b.actor_critic.named_parameters())
+    opt = torch.optim.Adam(a.actor_critic.parameters(), lr=3e-4)  # default (non-capturable) path
+    g = torch.Generator(device=DEV).manual_seed(5)
+    args = F._args(*([torch.zeros(1, device=DEV)] * 5), 0)
+    args.grads_modified = 1
+    for t in range(1, 6):
+        scale = 0.2 if t % 2 else 3.0  # alternate un-clipped / clipped steps
+        for name, p in pa.items():
+            gr = torch.randn(p.shape, device=DEV, generator=g) * scale
+            p.grad = gr.clone()
+            pb[name].grad.copy_(gr)
+        torch.nn.utils.clip_grad_norm_(a.actor_critic.parameters(), 0.5)
+        opt.step()
+        F.counters[0] = t
+        F._opt(args)
+        torch.cuda.synchronize()
+        for name in pa:
+            torch.testing.assert_close(pb[name], pa[name], rtol=1e-5, atol=1e-7, msg=name)
+
+
+def test_fused_state_roundtrip_to_torch_optimizer(tmp_path):
+    S, H = 60, 64
+    a, b = _agents(S, H)
+    s, z, lp, adv, ret, perm = _data(512, S, a)
+    F = FusedPPO(b, 128, 4, use_graphs=False)
+    F.run(s, z, lp, adv.clone(), ret.clone(), perm.clone())
+    b._fused = F
+    p = str(tmp_path / "ck.pth")
+    b.save(p)
+    ck = torch.load(p, weights_only=True)
+    assert set(ck) == {"model", "optimizer"}
+    st = ck["optimizer"]["state"]
+    assert len(st) == 13 and float(st[0]["step"]) == 2 * 4
+    # a fresh torch agent can resume from it
+    from ppo.agent import PPOAgent
+
+    c = PPOAgent(S, 2, hidden_dim=H, device=DEV, backend="torch")
+    c.load(p)
+    for (k, v1), (_, v2) in zip(b.actor_critic.state_dict().items(), c.actor_critic.state_dict().items()):
+        assert torch.equal(v1, v2), k
