@@ -25,7 +25,7 @@ namespace {
 
 constexpr int kTile = 64;
 constexpr int kKStep = 32;
-constexpr int kHeadRows = 64;  // minibatch rows per head workgroup (16 per wave)
+constexpr int kHeadRows = 16;  // minibatch rows per head workgroup (4 per wave)
 
 struct GemmArgs {
   int M, N, K;
@@ -153,19 +153,21 @@ __global__ void __launch_bounds__(256) gemm64(GemmArgs g) {
 // see); k-major operands (A transposed, B NN) are kept as [k][row] images (68-float pitch) and
 // read one k per MFMA.  Needs K % 4 == 0 for [row][k] operands and M, N % 4 == 0 otherwise.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr int kPitchRK = 36;  // [row][k] image: 144-B rows, conflict-free b128 reads
-constexpr int kPitchKR = 68;  // [k][row] image
+constexpr int kVK = 64;        // K-tile of the vector kernel: 8 16-byte loads per thread in flight
+constexpr int kPitchRK = 68;   // [row][k] image: 272-B rows, conflict-free ds_read_b128
+constexpr int kPitchKR = 68;   // [k][row] image
+constexpr int kV4 = kTile * kVK / 4 / 256;  // float4 per thread per operand per K-tile (4)
 
 template <int AM>
 __device__ __forceinline__ f32x4 load_a4(const GemmArgs& g, int e4, int m0, int k0, int kend) {
   f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f};
-  if (AM == A_ROW) {
-    const int r = e4 >> 3, k = k0 + (e4 & 7) * 4, m = m0 + r;
+  if (AM == A_ROW) {  // [row][k]: 16 float4 per 64-k row
+    const int r = e4 >> 4, k = k0 + (e4 & 15) * 4, m = m0 + r;
     if (m >= g.M || k >= kend) return z;
     const long row = g.a_gather ? (long)g.a_gather[m] : (long)m;
     return *reinterpret_cast<const f32x4*>(g.A + row * g.lda + k);
   }
-  const int k = k0 + (e4 >> 4), m = m0 + (e4 & 15) * 4;
+  const int k = k0 + (e4 >> 4), m = m0 + (e4 & 15) * 4;  // [k][row]: 16 float4 per 64-m row
   if (m >= g.M || k >= kend) return z;
   return *reinterpret_cast<const f32x4*>(g.A + (long)k * g.lda + m);
 }
@@ -174,7 +176,7 @@ template <int BM>
 __device__ __forceinline__ f32x4 load_b4(const GemmArgs& g, int e4, int n0, int k0, int kend) {
   f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f};
   if (BM == B_NT) {
-    const int r = e4 >> 3, k = k0 + (e4 & 7) * 4, n = n0 + r;
+    const int r = e4 >> 4, k = k0 + (e4 & 15) * 4, n = n0 + r;
     if (n >= g.N || k >= kend) return z;
     const float* p = n < g.split ? g.B + (long)n * g.ldb : g.B2 + (long)(n - g.split) * g.ldb;
     return *reinterpret_cast<const f32x4*>(p + k);
@@ -191,12 +193,16 @@ __device__ __forceinline__ f32x4 load_b4(const GemmArgs& g, int e4, int n0, int 
   return *reinterpret_cast<const f32x4*>(p + n);
 }
 
+// Same contract as gemm64 with 16-byte global loads, a 64-deep K-tile and LDS images in each
+// operand's natural layout.  Operands with k contiguous in memory (A row-major, B NT) become
+// [row][k] images read with ds_read_b128 (MFMA step s of lane half h uses k = 32h + s, a
+// permutation of the K-tile that the sum does not see); k-major operands (A transposed, B NN)
+// become [k][row] images read one k per MFMA.  Needs K % 4 == 0 for [row][k] operands and
+// M, N % 4 == 0 for [k][row] ones (launch_gemm falls back to gemm64 otherwise).
 template <int AM, int BM, int EPI>
 __global__ void __launch_bounds__(256) gemm64v(GemmArgs g) {
-  constexpr int A_SZ = AM == A_ROW ? kTile * kPitchRK : kKStep * kPitchKR;
-  constexpr int B_SZ = BM == B_NT ? kTile * kPitchRK : kKStep * kPitchKR;
-  __shared__ __attribute__((aligned(16))) float As[A_SZ];
-  __shared__ __attribute__((aligned(16))) float Bs[B_SZ];
+  __shared__ __attribute__((aligned(16))) float As[64 * kPitchRK];
+  __shared__ __attribute__((aligned(16))) float Bs[64 * kPitchRK];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, l32 = lane & 31;
   const int m0 = blockIdx.x * kTile, n0 = blockIdx.y * kTile;
   int kbeg = 0, kend = g.K;
@@ -208,57 +214,61 @@ __global__ void __launch_bounds__(256) gemm64v(GemmArgs g) {
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-  f32x4 ra[2], rb[2];
+  f32x4 ra[kV4], rb[kV4];
   float colsum = 0.0f;
   const bool do_colsum = EPI == EPI_SPLITK && g.bias_part && blockIdx.y == 0 && t < kTile;
   auto fetch = [&](int k0) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kV4; ++i) {
       ra[i] = load_a4<AM>(g, t + 256 * i, m0, k0, kend);
       rb[i] = load_b4<BM>(g, t + 256 * i, n0, k0, kend);
     }
   };
-  auto lds_off = [&](int am_mode_row, int e4) {
-    // [row][k]: row = e4>>3, k = (e4&7)*4 ; [k][row]: k = e4>>4, row = (e4&15)*4
-    return am_mode_row ? (e4 >> 3) * kPitchRK + (e4 & 7) * 4 : (e4 >> 4) * kPitchKR + (e4 & 15) * 4;
-  };
   if (kbeg < kend) fetch(kbeg);
-  for (int k0 = kbeg; k0 < kend; k0 += kKStep) {
+  for (int k0 = kbeg; k0 < kend; k0 += kVK) {
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kV4; ++i) {
       const int e4 = t + 256 * i;
-      *reinterpret_cast<f32x4*>(&As[lds_off(AM == A_ROW, e4)]) = ra[i];
-      *reinterpret_cast<f32x4*>(&Bs[lds_off(BM == B_NT, e4)]) = rb[i];
+      // both layouts: image row = e4 >> 4, column = (e4 & 15) * 4
+      const int off = (e4 >> 4) * kPitchRK + (e4 & 15) * 4;
+      *reinterpret_cast<f32x4*>(&As[off]) = ra[i];
+      *reinterpret_cast<f32x4*>(&Bs[off]) = rb[i];
     }
     __syncthreads();
-    if (k0 + kKStep < kend) fetch(k0 + kKStep);
-    float a[16], b[16];
-    if (AM == A_ROW) {
+    if (k0 + kVK < kend) fetch(k0 + kVK);  // next K-tile in flight during the MFMAs
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(&As[(wm + l32) * kPitchRK + h * 16 + 4 * q]);
-        a[4 * q] = v[0], a[4 * q + 1] = v[1], a[4 * q + 2] = v[2], a[4 * q + 3] = v[3];
+    for (int half = 0; half < 2; ++half) {
+      float a[16], b[16];
+      if (AM == A_ROW) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(
+              &As[(wm + l32) * kPitchRK + h * 32 + half * 16 + 4 * q]);
+          a[4 * q] = v[0], a[4 * q + 1] = v[1], a[4 * q + 2] = v[2], a[4 * q + 3] = v[3];
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < 16; ++s) a[s] = As[(h * 32 + half * 16 + s) * kPitchKR + wm + l32];
       }
-    } else {
+      if (BM == B_NT) {
 #pragma unroll
-      for (int s = 0; s < 16; ++s) a[s] = As[(h * 16 + s) * kPitchKR + wm + l32];
-    }
-    if (BM == B_NT) {
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(
+              &Bs[(wn + l32) * kPitchRK + h * 32 + half * 16 + 4 * q]);
+          b[4 * q] = v[0], b[4 * q + 1] = v[1], b[4 * q + 2] = v[2], b[4 * q + 3] = v[3];
+        }
+      } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(&Bs[(wn + l32) * kPitchRK + h * 16 + 4 * q]);
-        b[4 * q] = v[0], b[4 * q + 1] = v[1], b[4 * q + 2] = v[2], b[4 * q + 3] = v[3];
+        for (int s = 0; s < 16; ++s) b[s] = Bs[(h * 32 + half * 16 + s) * kPitchKR + wn + l32];
       }
-    } else {
 #pragma unroll
-      for (int s = 0; s < 16; ++s) b[s] = Bs[(h * 16 + s) * kPitchKR + wn + l32];
+      for (int s = 0; s < 16; ++s)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
     }
-#pragma unroll
-    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
     if (do_colsum) {
-#pragma unroll
-      for (int k = 0; k < kKStep; ++k) colsum += As[k * kPitchKR + t];
+#pragma unroll 8
+      for (int k = 0; k < kVK; ++k) colsum += As[k * kPitchKR + t];
     }
   }
 #pragma unroll
