@@ -41,6 +41,8 @@ static int pe_extra(const hwy_config* c) {
 static int validate(const hwy_config* c) {
   if (!c) return fail(HWY_EINVAL, "config is NULL");
   if (c->num_envs < 1) return fail(HWY_EINVAL, "num_envs must be >= 1, got %d", c->num_envs);
+  if (c->num_envs > (1 << 26) - 1)  // state words of one field indexed with 32 bits on device
+    return fail(HWY_EINVAL, "num_envs must be < 2^26 per handle, got %d", c->num_envs);
   if (c->lanes_count < 1 || c->lanes_count > 64)
     return fail(HWY_EINVAL, "lanes_count must be in [1, 64], got %d", c->lanes_count);
   if (c->vehicles_count < 0 || c->vehicles_count + 1 > HWY_MAX_VEHICLES)
@@ -258,7 +260,7 @@ int hwy_gae(const float* rewards, const uint8_t* dones, const float* values,
 }
 
 int hwy_math_selftest(int op, const float* in, const float* in2, float* out, int n, void* stream) {
-  if (op < 0 || op > 11 || n < 0) return fail(HWY_EINVAL, "bad selftest op %d", op);
+  if (op < 0 || op > 14 || n < 0) return fail(HWY_EINVAL, "bad selftest op %d", op);
   if (hwy_launch_math(op, in, in2, out, n, (hipStream_t)stream))
     return hip_fail(hipGetLastError(), "hwy_math_kernel");
   return HWY_OK;

@@ -68,6 +68,45 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// ------------------------------------------------------------------------- section clocks
+// Development build only (make prof -> libhwy_prof.so): per-section shader-clock totals of the
+// step kernel, summed over waves, read back with hwy_debug_sections().
+#define HWY_NSEC 16
+#ifdef HWY_SECTION_PROFILE
+__device__ unsigned long long g_hwy_sections[HWY_NSEC];
+struct SecProf {
+  uint64_t t;
+  uint64_t acc[HWY_NSEC];
+};
+#define SEC_START(sp)                                      \
+  do {                                                     \
+    (sp).t = __builtin_amdgcn_s_memtime();                 \
+    for (int _i = 0; _i < HWY_NSEC; ++_i) (sp).acc[_i] = 0; \
+  } while (0)
+#define SEC(sp, id)                                      \
+  do {                                                   \
+    const uint64_t _n = __builtin_amdgcn_s_memtime();    \
+    (sp).acc[id] += _n - (sp).t;                         \
+    (sp).t = _n;                                         \
+  } while (0)
+#define SEC_FLUSH(sp, lane)                                                        \
+  do {                                                                             \
+    if ((lane) == 0)                                                               \
+      for (int _i = 0; _i < HWY_NSEC; ++_i) atomicAdd(&g_hwy_sections[_i], (sp).acc[_i]); \
+  } while (0)
+#else
+struct SecProf {};
+#define SEC_START(sp) \
+  do {                \
+  } while (0)
+#define SEC(sp, id) \
+  do {              \
+  } while (0)
+#define SEC_FLUSH(sp, lane) \
+  do {                      \
+  } while (0)
+#endif
+
 // ------------------------------------------------------------------------- vehicle state
 struct Veh {
   float x, y, h, spd, tsp, dlt, tmr, ix, iy;
@@ -106,13 +145,30 @@ __device__ __forceinline__ float desired_gap(float a_spd, float a_c, float a_s, 
   return (DISTANCE_WANTED + a_spd * TIME_WANTED) + (a_spd * dv) / TWO_SQRT_AB;
 }
 
+// IDMVehicle.acceleration, free-road term (depends on the ego vehicle and DELTA only)
+__device__ __forceinline__ float idm_free(float ev_spd, float ev_tsp, float delta, float limit) {
+  float tsp = hm_clipf(ev_tsp, 0.0f, limit);
+  float base = hm_maxf(ev_spd, 0.0f) / hm_absf(hm_not_zero(tsp));
+  return COMFORT_ACC_MAX * (1.0f - hm_powf(base, delta));
+}
+
+// IDMVehicle.acceleration given its free-road term `acc` (interaction with the front vehicle)
+__device__ __forceinline__ float idm_with_front(float acc, float ev_spd, float ev_x, float ev_c,
+                                                float ev_s, bool has_front, float fv_x,
+                                                float fv_spd, float fv_c, float fv_s) {
+  if (has_front) {
+    float d = fv_x - ev_x;
+    float g = desired_gap(ev_spd, ev_c, ev_s, fv_spd, fv_c, fv_s) / hm_not_zero(d);
+    acc = acc - COMFORT_ACC_MAX * (g * g);
+  }
+  return acc;
+}
+
 // IDMVehicle.acceleration(ego_vehicle=ev, front_vehicle=fv) with the caller's DELTA
 __device__ __forceinline__ float idm_acc(float ev_spd, float ev_tsp, float ev_x, float ev_c,
                                          float ev_s, bool has_front, float fv_x, float fv_spd,
                                          float fv_c, float fv_s, float delta, float limit) {
-  float tsp = hm_clipf(ev_tsp, 0.0f, limit);
-  float base = hm_maxf(ev_spd, 0.0f) / hm_absf(hm_not_zero(tsp));
-  float acc = COMFORT_ACC_MAX * (1.0f - hm_powf(base, delta));
+  float acc = idm_free(ev_spd, ev_tsp, delta, limit);
   if (has_front) {
     float d = fv_x - ev_x;
     float g = desired_gap(ev_spd, ev_c, ev_s, fv_spd, fv_c, fv_s) / hm_not_zero(d);
@@ -132,76 +188,67 @@ __device__ __forceinline__ float steering_control(float y, float h, float spd, i
   float heading_rate_command = KP_HEADING * hm_wrap_to_pi(heading_ref - h);
   float slip_angle = hm_asinf(
       hm_clipf((VEH_LENGTH / 2.0f) / hm_not_zero(spd) * heading_rate_command, -1.0f, 1.0f));
-  float steering_angle = hm_atanf(2.0f * hm_tanf(slip_angle));
+  float steering_angle = hm_atanf(2.0f * hm_tanf_sc(slip_angle));
   return hm_clipf(steering_angle, -MAX_STEERING, MAX_STEERING);
 }
 
-// utils.are_polygons_intersecting on the two 5x2 m rectangles (a = lower road index)
-__device__ void sat_collide(float ax, float ay, float ac, float as, float dax, float day, float bx,
-                            float by, float bc, float bs, float dbx, float dby, bool* inter_out,
-                            bool* will_out, float* tx, float* ty) {
-  const float px[4] = {-VEH_LENGTH / 2.0f, -VEH_LENGTH / 2.0f, VEH_LENGTH / 2.0f, VEH_LENGTH / 2.0f};
-  const float py[4] = {-VEH_WIDTH / 2.0f, VEH_WIDTH / 2.0f, VEH_WIDTH / 2.0f, -VEH_WIDTH / 2.0f};
-  float A[5][2], B[5][2];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    A[k][0] = (ac * px[k] - as * py[k]) + ax;
-    A[k][1] = (as * px[k] + ac * py[k]) + ay;
-    B[k][0] = (bc * px[k] - bs * py[k]) + bx;
-    B[k][1] = (bs * px[k] + bc * py[k]) + by;
-  }
-  A[4][0] = A[0][0];
-  A[4][1] = A[0][1];
-  B[4][0] = B[0][0];
-  B[4][1] = B[0][1];
-  float cdx = (((A[0][0] + A[1][0]) + A[2][0]) + A[3][0]) / 4.0f -
-              (((B[0][0] + B[1][0]) + B[2][0]) + B[3][0]) / 4.0f;
-  float cdy = (((A[0][1] + A[1][1]) + A[2][1]) + A[3][1]) / 4.0f -
-              (((B[0][1] + B[1][1]) + B[2][1]) + B[3][1]) / 4.0f;
-  bool inter = true, will = true, stop = false;
+// utils.are_polygons_intersecting on the two 5x2 m rectangles (a = lower road index), in the
+// closed form of oracle/hwy_oracle.c rect_sat (same operations in the same order): intervals
+// centre.n -/+ (L/2 |u.n| + W/2 |v.n|) on upstream's eight edge normals
+// -u_a, v_a, u_a, -v_a, -u_b, v_b, u_b, -v_b, the opposite ones by exact negation.
+__device__ __forceinline__ void rect_interval(float x, float y, float c, float s, float nx,
+                                              float ny, float& mn, float& mx) {
+  const float p = x * nx + y * ny;
+  const float r = (VEH_LENGTH / 2.0f) * hm_absf(c * nx + s * ny) +
+                  (VEH_WIDTH / 2.0f) * hm_absf(c * ny - s * nx);
+  mn = p - r;
+  mx = p + r;
+}
+
+__device__ __forceinline__ float interval_distance(float min_a, float max_a, float min_b,
+                                                   float max_b) {
+  return min_a < min_b ? min_b - max_a : min_a - max_b;
+}
+
+__device__ __forceinline__ void sat_collide(float xa, float ya, float ca, float sa, float dax,
+                                            float day, float xb, float yb, float cb, float sb,
+                                            float dbx, float dby, bool* inter_out, bool* will_out,
+                                            float* tx, float* ty) {
+  const float cdx = xa - xb, cdy = ya - yb;
+  const float ddx = dax - dbx, ddy = day - dby;
+  bool inter = true, will = true;
   float min_distance = __builtin_huge_valf(), axx = 0.0f, axy = 0.0f;
+  float pa0[2], pa1[2], pb0[2], pb1[2], vpk[2], cdk[2], nxk[2], nyk[2];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const int k = e & 3;
-    float q1x = e < 4 ? A[k][0] : B[k][0], q1y = e < 4 ? A[k][1] : B[k][1];
-    float q2x = e < 4 ? A[k + 1][0] : B[k + 1][0], q2y = e < 4 ? A[k + 1][1] : B[k + 1][1];
-    if (k == 0) stop = false;  // upstream's `break` leaves only the inner (edge) loop
-    if (!stop) {
-      float nx = -q2y + q1y;
-      float ny = q2x - q1x;
-      float nn = __builtin_sqrtf(nx * nx + ny * ny);
-      nx = nx / nn;
-      ny = ny / nn;
-      float min_a = 0.0f, max_a = 0.0f, min_b = 0.0f, max_b = 0.0f;
-#pragma unroll
-      for (int p = 0; p < 5; ++p) {
-        float pa = A[p][0] * nx + A[p][1] * ny;
-        float pb = B[p][0] * nx + B[p][1] * ny;
-        if (p == 0 || pa < min_a) min_a = pa;
-        if (p == 0 || pa > max_a) max_a = pa;
-        if (p == 0 || pb < min_b) min_b = pb;
-        if (p == 0 || pb > max_b) max_b = pb;
-      }
-      float id0 = min_a < min_b ? min_b - max_a : min_a - max_b;
-      if (id0 > 0.0f) inter = false;
-      float vp = nx * (dax - dbx) + ny * (day - dby);
+    const int k = e & 1;
+    float min_a, max_a, min_b, max_b, vp, cd, sx, sy;
+    if (!(e & 2)) {  // -u (k = 0) or v (k = 1) of rectangle e / 4
+      const float c = e < 4 ? ca : cb, s = e < 4 ? sa : sb;
+      nxk[k] = k ? -s : -c;
+      nyk[k] = k ? c : -s;
+      rect_interval(xa, ya, ca, sa, nxk[k], nyk[k], pa0[k], pa1[k]);
+      rect_interval(xb, yb, cb, sb, nxk[k], nyk[k], pb0[k], pb1[k]);
+      vpk[k] = nxk[k] * ddx + nyk[k] * ddy;
+      cdk[k] = cdx * nxk[k] + cdy * nyk[k];
+      min_a = pa0[k], max_a = pa1[k], min_b = pb0[k], max_b = pb1[k];
+      vp = vpk[k], cd = cdk[k], sx = nxk[k], sy = nyk[k];
+    } else {  // the opposite edge: n -> -n
+      min_a = -pa1[k], max_a = -pa0[k], min_b = -pb1[k], max_b = -pb0[k];
+      vp = -vpk[k], cd = -cdk[k], sx = -nxk[k], sy = -nyk[k];
+    }
+    if (inter || will) {  // upstream breaks out once both are false
+      if (interval_distance(min_a, max_a, min_b, max_b) > 0.0f) inter = false;
       if (vp < 0.0f)
         min_a = min_a + vp;
       else
         max_a = max_a + vp;
-      float distance = min_a < min_b ? min_b - max_a : min_a - max_b;
+      const float distance = interval_distance(min_a, max_a, min_b, max_b);
       if (distance > 0.0f) will = false;
-      if (!inter && !will) {
-        stop = true;
-      } else if (hm_absf(distance) < min_distance) {
+      if ((inter || will) && hm_absf(distance) < min_distance) {
         min_distance = hm_absf(distance);
-        if (cdx * nx + cdy * ny > 0.0f) {
-          axx = nx;
-          axy = ny;
-        } else {
-          axx = -nx;
-          axy = -ny;
-        }
+        axx = cd > 0.0f ? sx : -sx;
+        axy = cd > 0.0f ? sy : -sy;
       }
     }
   }
@@ -422,20 +469,20 @@ __device__ void observe_wave(const hwy_config& C, int lane, const Veh& v, int st
 }
 
 // ------------------------------------------------------------------------- state I/O
-__device__ __forceinline__ void load_veh(const uint32_t* st, size_t fstride, size_t idx, int lane,
+__device__ __forceinline__ void load_veh(const uint32_t* st, size_t fstride, uint32_t idx, int lane,
                                          int V, Veh& v) {
-  v.x = hm_bits2f(st[HWY_F_X * fstride + idx]);
-  v.y = hm_bits2f(st[HWY_F_Y * fstride + idx]);
-  v.h = hm_bits2f(st[HWY_F_HEADING * fstride + idx]);
-  v.spd = hm_bits2f(st[HWY_F_SPEED * fstride + idx]);
-  v.tsp = hm_bits2f(st[HWY_F_TSPEED * fstride + idx]);
-  v.dlt = hm_bits2f(st[HWY_F_DELTA * fstride + idx]);
-  v.tmr = hm_bits2f(st[HWY_F_TIMER * fstride + idx]);
-  v.ix = hm_bits2f(st[HWY_F_IMPX * fstride + idx]);
-  v.iy = hm_bits2f(st[HWY_F_IMPY * fstride + idx]);
-  v.ln = (int)st[HWY_F_LANE * fstride + idx];
-  v.tl = (int)st[HWY_F_TLANE * fstride + idx];
-  uint32_t fl = st[HWY_F_FLAGS * fstride + idx];
+  v.x = hm_bits2f((st + HWY_F_X * fstride)[idx]);
+  v.y = hm_bits2f((st + HWY_F_Y * fstride)[idx]);
+  v.h = hm_bits2f((st + HWY_F_HEADING * fstride)[idx]);
+  v.spd = hm_bits2f((st + HWY_F_SPEED * fstride)[idx]);
+  v.tsp = hm_bits2f((st + HWY_F_TSPEED * fstride)[idx]);
+  v.dlt = hm_bits2f((st + HWY_F_DELTA * fstride)[idx]);
+  v.tmr = hm_bits2f((st + HWY_F_TIMER * fstride)[idx]);
+  v.ix = hm_bits2f((st + HWY_F_IMPX * fstride)[idx]);
+  v.iy = hm_bits2f((st + HWY_F_IMPY * fstride)[idx]);
+  v.ln = (int)(st + HWY_F_LANE * fstride)[idx];
+  v.tl = (int)(st + HWY_F_TLANE * fstride)[idx];
+  uint32_t fl = (st + HWY_F_FLAGS * fstride)[idx];
   v.crashed = (fl & HWY_FLAG_CRASHED) != 0u;
   v.imp = (fl & HWY_FLAG_IMPACT) != 0u;
   v.present = ((fl & HWY_FLAG_PRESENT) != 0u) && lane < V;
@@ -443,29 +490,33 @@ __device__ __forceinline__ void load_veh(const uint32_t* st, size_t fstride, siz
   v.asteer = 0.0f;
 }
 
-__device__ __forceinline__ void store_veh(uint32_t* st, size_t fstride, size_t idx, int lane, int V,
+__device__ __forceinline__ void store_veh(uint32_t* st, size_t fstride, uint32_t idx, int lane, int V,
                                           const Veh& v) {
+  // opaque copy of the offset: the 13 field addresses are rebuilt here instead of being kept
+  // live (26 VGPRs) from load_veh across the whole step
+  asm volatile("" : "+v"(idx));
   const bool live = lane < V;
-  st[HWY_F_X * fstride + idx] = live ? hm_f2bits(v.x) : 0u;
-  st[HWY_F_Y * fstride + idx] = live ? hm_f2bits(v.y) : 0u;
-  st[HWY_F_HEADING * fstride + idx] = live ? hm_f2bits(v.h) : 0u;
-  st[HWY_F_SPEED * fstride + idx] = live ? hm_f2bits(v.spd) : 0u;
-  st[HWY_F_TSPEED * fstride + idx] = live ? hm_f2bits(v.tsp) : 0u;
-  st[HWY_F_DELTA * fstride + idx] = live ? hm_f2bits(v.dlt) : 0u;
-  st[HWY_F_TIMER * fstride + idx] = live ? hm_f2bits(v.tmr) : 0u;
-  st[HWY_F_IMPX * fstride + idx] = (live && v.imp) ? hm_f2bits(v.ix) : 0u;
-  st[HWY_F_IMPY * fstride + idx] = (live && v.imp) ? hm_f2bits(v.iy) : 0u;
-  st[HWY_F_LANE * fstride + idx] = live ? (uint32_t)v.ln : 0u;
-  st[HWY_F_TLANE * fstride + idx] = live ? (uint32_t)v.tl : 0u;
-  st[HWY_F_FLAGS * fstride + idx] =
+  (st + HWY_F_X * fstride)[idx] = live ? hm_f2bits(v.x) : 0u;
+  (st + HWY_F_Y * fstride)[idx] = live ? hm_f2bits(v.y) : 0u;
+  (st + HWY_F_HEADING * fstride)[idx] = live ? hm_f2bits(v.h) : 0u;
+  (st + HWY_F_SPEED * fstride)[idx] = live ? hm_f2bits(v.spd) : 0u;
+  (st + HWY_F_TSPEED * fstride)[idx] = live ? hm_f2bits(v.tsp) : 0u;
+  (st + HWY_F_DELTA * fstride)[idx] = live ? hm_f2bits(v.dlt) : 0u;
+  (st + HWY_F_TIMER * fstride)[idx] = live ? hm_f2bits(v.tmr) : 0u;
+  (st + HWY_F_IMPX * fstride)[idx] = (live && v.imp) ? hm_f2bits(v.ix) : 0u;
+  (st + HWY_F_IMPY * fstride)[idx] = (live && v.imp) ? hm_f2bits(v.iy) : 0u;
+  (st + HWY_F_LANE * fstride)[idx] = live ? (uint32_t)v.ln : 0u;
+  (st + HWY_F_TLANE * fstride)[idx] = live ? (uint32_t)v.tl : 0u;
+  (st + HWY_F_FLAGS * fstride)[idx] =
       live ? ((v.crashed ? HWY_FLAG_CRASHED : 0u) | (v.imp ? HWY_FLAG_IMPACT : 0u) |
               (v.present ? HWY_FLAG_PRESENT : 0u))
            : 0u;
 }
 
-__device__ __forceinline__ void store_env_words(uint32_t* st, size_t fstride, size_t idx, int lane,
+__device__ __forceinline__ void store_env_words(uint32_t* st, size_t fstride, uint32_t idx, int lane,
                                                 int step, int episode, uint64_t seed, float ego_acc,
                                                 float ego_steer, float ep_return) {
+  asm volatile("" : "+v"(idx));
   uint32_t w = 0u;
   if (lane == HWY_E_STEP) w = (uint32_t)step;
   if (lane == HWY_E_EPISODE) w = (uint32_t)episode;
@@ -474,28 +525,107 @@ __device__ __forceinline__ void store_env_words(uint32_t* st, size_t fstride, si
   if (lane == HWY_E_EGO_ACC) w = hm_f2bits(ego_acc);
   if (lane == HWY_E_EGO_STEER) w = hm_f2bits(ego_steer);
   if (lane == HWY_E_RETURN) w = hm_f2bits(ep_return);
-  st[HWY_F_ENV * fstride + idx] = w;
+  (st + HWY_F_ENV * fstride)[idx] = w;
 }
 
-// ------------------------------------------------------------------------- one frame
-// Road.act() then Road.step(dt) for the env of this wave (lane = vehicle).
-__device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt) {
+// ------------------------------------------------------------------------- road order
+// The vehicles of a wave sorted by (x ascending, index descending), kept across the frames of
+// a step: lane p of `ord` holds the vehicle at position p, `rk` is this lane's position.
+// Absent lanes sort after every present vehicle, so the positions form a permutation of 0..63.
+struct RoadOrder {
+  int rk, ord;
+  bool valid;
+  bool tie;  // two present vehicles share an x, or an x is NaN (see road_order)
+};
+
+__device__ __forceinline__ uint64_t shf64(uint64_t v, int src) {
+  const uint32_t lo = (uint32_t)shi((int)(uint32_t)v, src);
+  const uint32_t hi = (uint32_t)shi((int)(uint32_t)(v >> 32), src);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// order-preserving u32 image of x (+0 and -0 map together); absent -> above every float
+__device__ __forceinline__ uint64_t road_key(float x, bool present, int lane) {
+  const uint32_t u = hm_f2bits(x + 0.0f);
+  uint32_t s = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  if (!present) s = 0xffffffffu;
+  return ((uint64_t)s << 32) | (uint32_t)(WAVE - 1 - lane);
+}
+
+// Re-validates (or rebuilds) the order for the current positions.  Sets o.tie when two
+// present vehicles share an x or an x is NaN: the callers then take the sequential scans, whose
+// tie-breaking the bit-mask neighbour search below does not reproduce.
+__device__ void road_order(int lane, const Veh& v, uint64_t pres, RoadOrder& o) {
+  const uint64_t key = road_key(v.x, v.present, lane);
+  const int nxt = lane < WAVE - 1 ? lane + 1 : lane;
+  uint64_t kp = 0ull, kn = 0ull;
+  bool sorted = false;
+  if (o.valid) {
+    kp = shf64(key, o.ord);
+    kn = shf64(kp, nxt);
+    sorted = !wave_any(lane < WAVE - 1 && !(kp < kn));
+  }
+  if (!sorted) {
+    int r = 0;
+    if (v.present) {
+      for (int k = 0; k < WAVE; ++k) {
+        if (!((pres >> k) & 1ull)) continue;
+        const uint64_t kk = ((uint64_t)(uint32_t)rdli((int)(key >> 32), k) << 32) |
+                            (uint32_t)(WAVE - 1 - k);
+        r += kk < key ? 1 : 0;
+      }
+    } else {  // absent lanes: after all present ones, by descending lane index
+      const uint64_t above = lane >= WAVE - 1 ? 0ull : (~0ull << (lane + 1));
+      r = __popcll(pres) + __popcll(~pres & above);
+    }
+    o.rk = r;
+    o.ord = __builtin_amdgcn_ds_permute(r << 2, lane);
+    o.valid = true;
+    kp = shf64(key, o.ord);
+    kn = shf64(kp, nxt);
+  }
+  const int npres = __popcll(pres);
+  const bool tie = lane + 1 < npres && (uint32_t)(kp >> 32) == (uint32_t)(kn >> 32);
+  o.tie = wave_any(tie || (v.present && v.x != v.x));
+}
+
+// Road.neighbour_vehicles(self, lane c) for c = ln-1, ln, ln+1 (slot s <-> c = ln-1+s) from the
+// road order: for each lane c a 64-bit mask over positions of the vehicles with
+// on_lane(c, margin 1); the front vehicle is the next set position above this one, the rear
+// the previous set position below (exact while no two x are equal, see road_order).
+__device__ __forceinline__ void neighbours_ordered(const hwy_config& C, int lane, const Veh& v,
+                                                   uint64_t pres, const RoadOrder& o, int fi[3],
+                                                   int ri[3]) {
+  const int npres = __popcll(pres);
+  const float xp = shf(v.x, o.ord), yp = shf(v.y, o.ord);
+  const bool okp = lane < npres && -LANE_VEH_LEN <= xp && xp < ROAD_LENGTH + LANE_VEH_LEN;
+  uint64_t m[3] = {0ull, 0ull, 0ull};
+  for (int c = 0; c < C.lanes_count; ++c) {
+    const uint64_t mc = ballot(okp && hm_absf(lane_lat(yp, c)) <= LANE_WIDTH / 2.0f + 1.0f);
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+      if (c == v.ln - 1 + s) m[s] = mc;
+  }
+  const uint64_t above = o.rk >= WAVE - 1 ? 0ull : (~0ull << (o.rk + 1));
+  const uint64_t below = (1ull << o.rk) - 1ull;
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    const uint64_t fa = m[s] & above, rb = m[s] & below;
+    const int qf = fa ? __builtin_ctzll(fa) : 0;
+    const int qr = rb ? 63 - __builtin_clzll(rb) : 0;
+    const int vf = shi(o.ord, qf), vr = shi(o.ord, qr);
+    fi[s] = fa ? vf : -1;
+    ri[s] = rb ? vr : -1;
+  }
+}
+
+// the same query by the sequential definition (one pass over the vehicles in index order)
+__device__ __forceinline__ void neighbours_scan(const hwy_config& C, int lane, const Veh& v,
+                                             uint64_t pres, int fi[3], int ri[3]) {
   const int V = C.vehicles_count + 1;
-  const int lanes = C.lanes_count;
-  const float limit = C.speed_limit;
-  const float ch = hm_cosf(v.h), sh = hm_sinf(v.h);
-  const uint64_t pres = ballot(v.present);
-
-  // ---------------- Road.act: IDMVehicle.act for every non-crashed traffic car
-  const bool actor = v.present && lane >= 1 && !v.crashed;
-  const int tl_old = v.tl;
-  const bool mid = v.ln != v.tl;
-  const bool fire = actor && !mid && (LANE_CHANGE_DELAY < v.tmr);  // utils.do_every
-  if (fire) v.tmr = 0.0f;
-
-  // Road.neighbour_vehicles on lanes ln-1, ln, ln+1 in one pass (slot s <-> lane ln-1+s)
-  int fi[3] = {-1, -1, -1}, ri[3] = {-1, -1, -1};
   float fsv[3] = {0.0f, 0.0f, 0.0f}, rsv[3] = {0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int s = 0; s < 3; ++s) fi[s] = ri[s] = -1;
   for (int k = 0; k < V; ++k) {
     if (!((pres >> k) & 1ull)) continue;
     const float xk = rdlf(v.x, k), yk = rdlf(v.y, k);
@@ -513,6 +643,42 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt) {
       }
     }
   }
+}
+
+// per-wave LDS of the collision pass (5.2 KB)
+struct CollLds {
+  unsigned long long imx[WAVE], imy[WAVE];  // (partner + 1) << 32 | impact bits, max-reduced
+  int crash[WAVE];
+  uint16_t plist[WAVE * (WAVE - 1) / 2];  // candidate pairs (a << 8 | b), a < b
+};
+
+// ------------------------------------------------------------------------- one frame
+// Road.act() then Road.step(dt) for the env of this wave (lane = vehicle).
+__device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, RoadOrder& ro,
+                           float& cos_h, float& sin_h, CollLds& cl, SecProf& sp) {
+  const int V = C.vehicles_count + 1;
+  const int lanes = C.lanes_count;
+  const float limit = C.speed_limit;
+  const float ch = cos_h, sh = sin_h;  // cos / sin of v.h (carried from the previous frame)
+  const uint64_t pres = ballot(v.present);
+
+  // ---------------- Road.act: IDMVehicle.act for every non-crashed traffic car
+  const bool actor = v.present && lane >= 1 && !v.crashed;
+  const int tl_old = v.tl;
+  const bool mid = v.ln != v.tl;
+  const bool fire = actor && !mid && (LANE_CHANGE_DELAY < v.tmr);  // utils.do_every
+  if (fire) v.tmr = 0.0f;
+
+  // Road.neighbour_vehicles on lanes ln-1, ln, ln+1 (slot s <-> lane ln-1+s)
+  int fi[3], ri[3];
+  SEC(sp, 0);
+  if (!ro.valid) road_order(lane, v, pres, ro);  // later frames: validated after the last move
+  SEC(sp, 9);
+  if (ro.tie)
+    neighbours_scan(C, lane, v, pres, fi, ri);
+  else
+    neighbours_ordered(C, lane, v, pres, ro, fi, ri);
+  SEC(sp, 1);
 
   // gathers (all lanes active)
   const int sop = fi[1] >= 0 ? fi[1] : lane;
@@ -538,11 +704,16 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt) {
 
   // acceleration(self, front on own lane): IDM term and MOBIL's self_a
   float self_a = 0.0f;
-  if (actor)
-    self_a = idm_acc(v.spd, v.tsp, v.x, ch, sh, fi[1] >= 0, op_x, op_spd, op_c, op_s, v.dlt, limit);
+  // (the free-road term is shared by every acceleration(self, .) evaluated this frame)
+  float a_free = 0.0f;
+  if (actor) {
+    a_free = idm_free(v.spd, v.tsp, v.dlt, limit);
+    self_a = idm_with_front(a_free, v.spd, v.x, ch, sh, fi[1] >= 0, op_x, op_spd, op_c, op_s);
+  }
 
   // IDMVehicle.change_lane_policy -> mobil, side lanes left then right (POLITENESS = 0, so the
   // followers' unchanged-lane terms multiply by zero and are not evaluated)
+  SEC(sp, 2);
   int ntl = v.tl;
   if (fire) {
 #pragma unroll
@@ -559,13 +730,14 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt) {
         nfp = idm_acc(nf_spd[q], nf_tsp[q], nf_x[q], nf_c[q], nf_s[q], true, v.x, v.spd, ch, sh,
                       v.dlt, limit);
       if (nfp < -LANE_CHANGE_MAX_BRAKING_IMPOSED) continue;
-      const float spa = idm_acc(v.spd, v.tsp, v.x, ch, sh, fi[s] >= 0, np_x[q], np_spd[q], np_c[q],
-                                np_s[q], v.dlt, limit);
+      const float spa = idm_with_front(a_free, v.spd, v.x, ch, sh, fi[s] >= 0, np_x[q],
+                                       np_spd[q], np_c[q], np_s[q]);
       if ((spa - self_a) < LANE_CHANGE_MIN_ACC_GAIN) continue;
       ntl = c;
     }
   }
 
+  SEC(sp, 3);
   // abort an ongoing lane change if another car targets the same lane within its desired gap,
   // in road order (lower indices already final, higher ones at their frame-start target)
   int tl_cur = ntl;
@@ -584,6 +756,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt) {
   }
   v.tl = tl_cur;
 
+  SEC(sp, 4);
   // IDM on the target lane while changing lanes
   const bool need_t = actor && v.ln != v.tl;
   int ft = -1;
@@ -614,7 +787,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt) {
     float acc = self_a;
     if (need_t) {
       const float acc_t =
-          idm_acc(v.spd, v.tsp, v.x, ch, sh, ft >= 0, ft_x, ft_spd, ft_c, ft_s, v.dlt, limit);
+          idm_with_front(a_free, v.spd, v.x, ch, sh, ft >= 0, ft_x, ft_spd, ft_c, ft_s);
       acc = hm_minf(acc, acc_t);
     }
     acc = hm_clipf(acc, -ACC_MAX, ACC_MAX);
@@ -622,6 +795,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt) {
     v.aacc = acc;
   }
 
+  SEC(sp, 5);
   // ---------------- Road.step: Vehicle.step for every vehicle
   if (v.present) {
     if (lane != 0) v.tmr = v.tmr + dt;  // IDMVehicle.step
@@ -634,9 +808,11 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt) {
     } else if (v.spd < MIN_SPEED) {
       v.aacc = hm_maxf(v.aacc, 1.0f * (MIN_SPEED - v.spd));
     }
-    const float beta = hm_atanf(0.5f * hm_tanf(v.asteer));
-    const float vx = v.spd * hm_cosf(v.h + beta);
-    const float vy = v.spd * hm_sinf(v.h + beta);
+    const float beta = hm_atanf(0.5f * hm_tanf_sc(v.asteer));
+    float sdir, cdir;
+    hm_sincosf(v.h + beta, &sdir, &cdir);
+    const float vx = v.spd * cdir;
+    const float vy = v.spd * sdir;
     v.x = v.x + vx * dt;
     v.y = v.y + vy * dt;
     if (v.imp) {
@@ -650,51 +826,120 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt) {
     v.ln = closest_lane(v.y, lanes);  // on_state_update
   }
 
+  SEC(sp, 6);
   // ---------------- Road.step: handle_collisions for every pair, a = lower index
-  const float c2 = hm_cosf(v.h), s2 = hm_sinf(v.h);
-  const float dax_self = (v.spd * c2) * dt, day_self = (v.spd * s2) * dt;
+  float c2, s2;
+  hm_sincosf(v.h, &s2, &c2);
+  cos_h = c2;
+  sin_h = s2;
+  road_order(lane, v, pres, ro);  // new positions; also serves the next frame's neighbours
+  SEC(sp, 7);
+  // Candidates first: a pair can pass the centre-distance pre-check only if |dx| is within
+  // that bound, taken here with the wave's largest speed (and widened past any rounding; a
+  // non-finite speed or position disables the filter).
+  float vabs = v.present ? hm_absf(v.spd) : 0.0f;
+  bool nonfinite = v.present && !(hm_absf(v.x) <= 3.0e38f && hm_absf(v.y) <= 3.0e38f &&
+                                  hm_absf(v.spd) <= 3.0e38f);
+#pragma unroll
+  for (int m = 1; m < WAVE; m <<= 1) vabs = hm_maxf(vabs, shf(vabs, lane ^ m));
+  const float xbound = wave_any(nonfinite) ? __builtin_huge_valf()
+                                           : (VEH_DIAGONAL + vabs * dt) * 1.001f + 1.0e-3f;
   uint64_t pm = 0ull;
-  for (int k = 0; k < V; ++k) {
-    if (!((pres >> k) & 1ull)) continue;
-    const float xk = rdlf(v.x, k), yk = rdlf(v.y, k), vk = rdlf(v.spd, k);
-    const bool lower = lane < k;
-    const float dx = lower ? (xk - v.x) : (v.x - xk);
-    const float dy = lower ? (yk - v.y) : (v.y - yk);
-    const float va = lower ? v.spd : vk;
-    const bool pass = v.present && k != lane &&
-                      !(__builtin_sqrtf(dx * dx + dy * dy) >
-                        (VEH_DIAGONAL + VEH_DIAGONAL) / 2.0f + va * dt);
-    if (pass) pm |= (1ull << k);
-  }
-  while (wave_any(pm != 0ull)) {
-    const bool has = pm != 0ull;
-    const int j = has ? __builtin_ctzll(pm) : lane;
-    if (has) pm &= pm - 1ull;
-    const float xj = shf(v.x, j), yj = shf(v.y, j), cj = shf(c2, j), sj = shf(s2, j),
-                vj = shf(v.spd, j);
-    const float daxj = (vj * cj) * dt, dayj = (vj * sj) * dt;
-    const bool lower = lane < j;
-    bool inter, will;
-    float tx, ty;
-    sat_collide(lower ? v.x : xj, lower ? v.y : yj, lower ? c2 : cj, lower ? s2 : sj,
-                lower ? dax_self : daxj, lower ? day_self : dayj, lower ? xj : v.x,
-                lower ? yj : v.y, lower ? cj : c2, lower ? sj : s2, lower ? daxj : dax_self,
-                lower ? dayj : day_self, &inter, &will, &tx, &ty);
-    if (has) {
-      if (will) {
-        v.ix = lower ? tx / 2.0f : -tx / 2.0f;
-        v.iy = lower ? ty / 2.0f : -ty / 2.0f;
-        v.imp = true;
-      }
-      if (inter) v.crashed = true;
+  if (!ro.tie) {
+    // x-sorted road order: the candidates of a vehicle are the run of positions around its
+    // own whose |dx| stays within the bound; walk both ways until every lane has left its run
+    const int npres = __popcll(pres);
+    const float xs = shf(v.x, ro.ord);  // x at position `lane`
+    bool up = v.present, dn = v.present;
+    for (int o = 1; wave_any(up || dn); ++o) {
+      const int pu = ro.rk + o < WAVE ? ro.rk + o : WAVE - 1;
+      const int pd = ro.rk - o >= 0 ? ro.rk - o : 0;
+      const float xu = shf(xs, pu), xd = shf(xs, pd);
+      const int iu = shi(ro.ord, pu), id = shi(ro.ord, pd);
+      up = up && ro.rk + o < npres && !(hm_absf(xu - v.x) > xbound);
+      dn = dn && ro.rk - o >= 0 && !(hm_absf(xd - v.x) > xbound);
+      if (up) pm |= 1ull << iu;
+      if (dn) pm |= 1ull << id;
+    }
+  } else {
+    // |dx| is symmetric in the pair, so the ballot over lanes for vehicle k is k's own row
+    for (int k = 0; k < V; ++k) {
+      if (!((pres >> k) & 1ull)) continue;
+      const float xk = rdlf(v.x, k);
+      const uint64_t row = ballot(v.present && k != lane && !(hm_absf(xk - v.x) > xbound));
+      if (lane == k) pm = row;
     }
   }
+  SEC(sp, 10);
+  // Each candidate pair {i < j} once, spread over the lanes: lane i lists its pairs at its
+  // exclusive prefix offset, then lane t takes pair t (64 per round).  Per vehicle, upstream
+  // keeps the impact of its highest-index partner (the last handle_collisions call that writes
+  // it) and ORs the crash flag; the translation therefore goes through a 64-bit LDS max keyed
+  // by (partner + 1) in the high word.
+  uint64_t own = pm & (lane >= WAVE - 1 ? 0ull : (~0ull << (lane + 1)));
+  const int cnt = __popcll(own);
+  int off = cnt;  // inclusive scan of cnt over lanes
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    const int t = shi(off, lane >= d ? lane - d : lane);
+    if (lane >= d) off += t;
+  }
+  const int total = rdli(off, WAVE - 1);
+  off -= cnt;
+  cl.imx[lane] = 0ull;
+  cl.imy[lane] = 0ull;
+  cl.crash[lane] = 0;
+  while (own) {
+    const int j = __builtin_ctzll(own);
+    own &= own - 1ull;
+    cl.plist[off++] = (uint16_t)((lane << 8) | j);
+  }
+  wave_lds_sync();
+  for (int base = 0; base < total; base += WAVE) {
+    const bool has = base + lane < total;
+    const int pr = has ? cl.plist[base + lane] : 0;
+    const int a = pr >> 8, b = pr & 0xff;  // a < b
+    const float xa = shf(v.x, a), ya = shf(v.y, a), ca = shf(c2, a), sa = shf(s2, a),
+                va = shf(v.spd, a);
+    const float xb = shf(v.x, b), yb = shf(v.y, b), cb = shf(c2, b), sb = shf(s2, b),
+                vb = shf(v.spd, b);
+    // exact pre-check (are_polygons_intersecting is only called inside it), then the SAT test
+    const float dx = xb - xa, dy = yb - ya;
+    const bool pass = has && !(__builtin_sqrtf(dx * dx + dy * dy) >
+                               (VEH_DIAGONAL + VEH_DIAGONAL) / 2.0f + va * dt);
+    if (!wave_any(pass)) continue;
+    bool inter, will;
+    float tx, ty;
+    sat_collide(xa, ya, ca, sa, (va * ca) * dt, (va * sa) * dt, xb, yb, cb, sb, (vb * cb) * dt,
+                (vb * sb) * dt, &inter, &will, &tx, &ty);
+    if (pass && will) {
+      atomicMax(&cl.imx[a], ((uint64_t)(b + 1) << 32) | hm_f2bits(tx / 2.0f));
+      atomicMax(&cl.imy[a], ((uint64_t)(b + 1) << 32) | hm_f2bits(ty / 2.0f));
+      atomicMax(&cl.imx[b], ((uint64_t)(a + 1) << 32) | hm_f2bits(-tx / 2.0f));
+      atomicMax(&cl.imy[b], ((uint64_t)(a + 1) << 32) | hm_f2bits(-ty / 2.0f));
+    }
+    if (pass && inter) {
+      cl.crash[a] = 1;
+      cl.crash[b] = 1;
+    }
+  }
+  wave_lds_sync();
+  const uint64_t mx = cl.imx[lane], my = cl.imy[lane];
+  if (mx != 0ull) {
+    v.ix = hm_bits2f((uint32_t)mx);
+    v.iy = hm_bits2f((uint32_t)my);
+    v.imp = true;
+  }
+  if (cl.crash[lane]) v.crashed = true;
+  wave_lds_sync();  // the lists are rewritten next frame
+  SEC(sp, 8);
 }
 
 // ------------------------------------------------------------------------- kernels
 __global__ void __launch_bounds__(256, 4) hwy_step_kernel(StepParams P) {
   __shared__ int lds_vor[ENVS_PER_BLOCK][WAVE];
   __shared__ int lds_inv[ENVS_PER_BLOCK][WAVE];
+  __shared__ CollLds lds_coll[ENVS_PER_BLOCK];
   const hwy_config& C = P.cfg;
   const int lane = threadIdx.x & (WAVE - 1);
   const int w = threadIdx.x / WAVE;
@@ -702,12 +947,14 @@ __global__ void __launch_bounds__(256, 4) hwy_step_kernel(StepParams P) {
   if (e >= C.num_envs) return;  // whole wave
   const int V = C.vehicles_count + 1;
   const size_t fstride = (size_t)C.num_envs * WAVE;
-  const size_t idx = (size_t)e * WAVE + lane;
+  const uint32_t idx = (uint32_t)e * WAVE + lane;  // < 2^32: hwy_create bounds num_envs
   uint32_t* st = P.state;
 
+  SecProf sp;
+  SEC_START(sp);
   Veh v;
   load_veh(st, fstride, idx, lane, V, v);
-  const uint32_t ew = st[HWY_F_ENV * fstride + idx];
+  const uint32_t ew = (st + HWY_F_ENV * fstride)[idx];
   int step = rdli((int)ew, HWY_E_STEP);
   int episode = rdli((int)ew, HWY_E_EPISODE);
   uint64_t seed = (uint64_t)(uint32_t)rdli((int)ew, HWY_E_SEED_LO) |
@@ -721,14 +968,23 @@ __global__ void __launch_bounds__(256, 4) hwy_step_kernel(StepParams P) {
   const float dt = 1.0f / (float)C.sim_freq;
   const int frames = C.sim_freq / C.policy_freq;
   const float a0 = P.actions[2 * (size_t)e], a1 = P.actions[2 * (size_t)e + 1];
+  RoadOrder ro;
+  ro.rk = lane;
+  ro.ord = lane;
+  ro.valid = false;
+  ro.tie = false;
+  float cos_h, sin_h;
+  hm_sincosf(v.h, &sin_h, &cos_h);
+  SEC(sp, 15);
   for (int frame = 0; frame < frames; ++frame) {
     if (frame == 0 && lane == 0) {  // ContinuousAction.act
       v.aacc = hm_lmap(hm_clipf(a0, -1.0f, 1.0f), -1.0f, 1.0f, -5.0f, 5.0f);
       v.asteer = hm_lmap(hm_clipf(a1, -1.0f, 1.0f), -1.0f, 1.0f, -HM_PIO4_F, HM_PIO4_F);
     }
-    frame_wave(C, lane, v, dt);
+    frame_wave(C, lane, v, dt, ro, cos_h, sin_h, lds_coll[w], sp);
   }
   step += 1;
+  SEC(sp, 11);
 
   // HighwayEnv._reward / _is_terminated / _is_truncated on the ego (lane 0)
   float rew = 0.0f;
@@ -765,6 +1021,7 @@ __global__ void __launch_bounds__(256, 4) hwy_step_kernel(StepParams P) {
     if (P.ep_ret) P.ep_ret[e] = done ? ep_return : 0.0f;
     if (P.ep_len) P.ep_len[e] = done ? step : 0;
   }
+  SEC(sp, 11);
   if (done && C.autoreset) {
     episode += 1;
     seed = schedule_seed(C, e, episode);
@@ -772,11 +1029,15 @@ __global__ void __launch_bounds__(256, 4) hwy_step_kernel(StepParams P) {
     step = 0;
     ep_return = 0.0f;
   }
+  SEC(sp, 12);
   observe_wave(C, lane, v, step, seed, P.pe_table, P.obs + (size_t)e * C.obs_vehicles * P.fout,
                P.fout, lds_vor[w], lds_inv[w]);
+  SEC(sp, 13);
   store_veh(st, fstride, idx, lane, V, v);
   store_env_words(st, fstride, idx, lane, step, episode, seed, rdlf(v.aacc, 0), rdlf(v.asteer, 0),
                   ep_return);
+  SEC(sp, 14);
+  SEC_FLUSH(sp, lane);
 }
 
 __global__ void __launch_bounds__(256) hwy_reset_kernel(StepParams P) {
@@ -790,7 +1051,7 @@ __global__ void __launch_bounds__(256) hwy_reset_kernel(StepParams P) {
   if (P.mask && !P.mask[e]) return;
   const int V = C.vehicles_count + 1;
   const size_t fstride = (size_t)C.num_envs * WAVE;
-  const size_t idx = (size_t)e * WAVE + lane;
+  const uint32_t idx = (uint32_t)e * WAVE + lane;  // < 2^32: hwy_create bounds num_envs
   const uint64_t seed = P.seeds ? P.seeds[e] : schedule_seed(C, e, 0);
   Veh v;
   reset_wave(C, lane, seed, v);
@@ -865,6 +1126,9 @@ __global__ void hwy_math_kernel(int op, const float* in, const float* in2, float
     case 9: r = __builtin_sqrtf(x); break;
     case 10: r = x / y; break;
     case 11: r = hm_floorf(x); break;
+    case 12: { float c_; hm_sincosf(x, &r, &c_); } break;
+    case 13: { float s_; hm_sincosf(x, &s_, &r); } break;
+    case 14: r = hm_tanf_sc(x); break;
   }
   out[i] = r;
 }
@@ -904,3 +1168,16 @@ int hwy_launch_math(int op, const float* in, const float* in2, float* out, int n
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }
+
+#ifdef HWY_SECTION_PROFILE
+// development build only: copy out (and optionally clear) the section clock totals
+extern "C" int hwy_debug_sections(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hwy_sections), sizeof(g_hwy_sections)) != hipSuccess)
+    return -2;
+  if (reset) {
+    unsigned long long z[HWY_NSEC] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_hwy_sections), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return 0;
+}
+#endif

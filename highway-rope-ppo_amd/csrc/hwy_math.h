@@ -136,6 +136,61 @@ HWY_HD float hm_sinf(float x) { return hm_sincos_core(x, 0); }
 HWY_HD float hm_cosf(float x) { return hm_sincos_core(x, 1); }
 HWY_HD float hm_tanf(float x) { return hm_sinf(x) / hm_cosf(x); }
 
+/* hm_sinf(x) and hm_cosf(x) from one range reduction (bit-identical to the two calls). */
+HWY_HD void hm_sincosf(float xx, float* s_out, float* c_out) {
+  const float FOPI = 1.27323954473516f;
+  const float DP1 = 0.78515625f;
+  const float DP2 = 2.4187564849853515625e-4f;
+  const float DP3 = 3.77489497744594108e-8f;
+  float x = xx;
+  int sign_s = 1, sign_c = 1;
+  if (x < 0.0f) {
+    x = -x;
+    sign_s = -1;
+  }
+  if (!(x <= 16777215.0f)) {
+    const float r = hm_isnan(x) ? x : 0.0f;
+    *s_out = r;
+    *c_out = r;
+    return;
+  }
+  uint32_t j = (uint32_t)(FOPI * x);
+  float y = (float)j;
+  if (j & 1u) {
+    j += 1u;
+    y += 1.0f;
+  }
+  j &= 7u;
+  if (j > 3u) {
+    sign_s = -sign_s;
+    sign_c = -sign_c;
+    j -= 4u;
+  }
+  if (j > 1u) sign_c = -sign_c;
+  x = ((x - y * DP1) - y * DP2) - y * DP3;
+  const float z = x * x;
+  float rc = 2.443315711809948E-005f;
+  rc = rc * z - 1.388731625493765E-003f;
+  rc = rc * z + 4.166664568298827E-002f;
+  rc = rc * (z * z);
+  rc = rc - 0.5f * z;
+  rc = rc + 1.0f;
+  float rs = -1.9515295891E-4f;
+  rs = rs * z + 8.3321608736E-3f;
+  rs = rs * z - 1.6666654611E-1f;
+  rs = rs * (z * x);
+  rs = rs + x;
+  const int swap = (j == 1u || j == 2u);
+  const float s = swap ? rc : rs, c = swap ? rs : rc;
+  *s_out = sign_s < 0 ? -s : s;
+  *c_out = sign_c < 0 ? -c : c;
+}
+HWY_HD float hm_tanf_sc(float x) {
+  float s, c;
+  hm_sincosf(x, &s, &c);
+  return s / c;
+}
+
 /* Cephes atanf */
 HWY_HD float hm_atanf(float xx) {
   float x = xx, y;

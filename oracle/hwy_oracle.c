@@ -428,6 +428,103 @@ static void are_polygons_intersecting(float A[5][2], float B[5][2], float dax, f
   *ty = will ? min_distance * axy : 0.0f;
 }
 
+/* are_polygons_intersecting on two vehicle rectangles in closed form -- the form the simulation
+ * uses (deliberate deviation).  Rectangle: centre (x, y), heading unit vector
+ * u = (c, s), v = (-s, c), half extents L/2 and W/2, so its interval on axis n is
+ * centre.n -/+ (L/2 |u.n| + W/2 |v.n|).  Upstream's eight edge normals, in its order, are
+ * -u_a, v_a, u_a, -v_a, -u_b, v_b, u_b, -v_b: the intervals are computed for the first two of
+ * each rectangle and negated (exactly) for the opposite ones; the break and tie rules are
+ * upstream's.  The centre difference is taken from the centres (upstream: the mean of the
+ * corners).  Equal to are_polygons_intersecting() above up to binary32 rounding:
+ * hwyo_sat_compare / tests/test_oracle_env.py. */
+static void rect_interval(float x, float y, float c, float s, float nx, float ny, float* mn,
+                          float* mx) {
+  float p = x * nx + y * ny;
+  float r = (VEH_LENGTH / 2.0f) * hm_absf(c * nx + s * ny) +
+            (VEH_WIDTH / 2.0f) * hm_absf(c * ny - s * nx);
+  *mn = p - r;
+  *mx = p + r;
+}
+
+static void rect_sat(float xa, float ya, float ca, float sa, float dax, float day, float xb,
+                     float yb, float cb, float sb, float dbx, float dby, int* intersecting,
+                     int* will_intersect, float* tx, float* ty) {
+  const float cdx = xa - xb, cdy = ya - yb;
+  const float ddx = dax - dbx, ddy = day - dby;
+  int inter = 1, will = 1;
+  float min_distance = INFINITY, axx = 0.0f, axy = 0.0f;
+  for (int e = 0; e < 8 && (inter || will); ++e) {
+    const int k = e & 1;              /* -u or v of rectangle e / 4 */
+    const float c = e < 4 ? ca : cb, s = e < 4 ? sa : sb;
+    const float nx = k ? -s : -c, ny = k ? c : -s;
+    float min_a, max_a, min_b, max_b;
+    rect_interval(xa, ya, ca, sa, nx, ny, &min_a, &max_a);
+    rect_interval(xb, yb, cb, sb, nx, ny, &min_b, &max_b);
+    float vp = nx * ddx + ny * ddy;
+    float cd = cdx * nx + cdy * ny;
+    float sx = nx, sy = ny;
+    if (e & 2) { /* the opposite edge: n -> -n */
+      float t = min_a;
+      min_a = -max_a;
+      max_a = -t;
+      t = min_b;
+      min_b = -max_b;
+      max_b = -t;
+      vp = -vp;
+      cd = -cd;
+      sx = -nx;
+      sy = -ny;
+    }
+    if (interval_distance(min_a, max_a, min_b, max_b) > 0.0f) inter = 0;
+    if (vp < 0.0f)
+      min_a = min_a + vp;
+    else
+      max_a = max_a + vp;
+    float distance = interval_distance(min_a, max_a, min_b, max_b);
+    if (distance > 0.0f) will = 0;
+    if (!inter && !will) break;
+    if (hm_absf(distance) < min_distance) {
+      min_distance = hm_absf(distance);
+      if (cd > 0.0f) {
+        axx = sx;
+        axy = sy;
+      } else {
+        axx = -sx;
+        axy = -sy;
+      }
+    }
+  }
+  *intersecting = inter;
+  *will_intersect = will;
+  *tx = will ? min_distance * axx : 0.0f;
+  *ty = will ? min_distance * axy : 0.0f;
+}
+
+/* Both forms on the same pairs (test hook).  in[n][12] = xa ya ha spa xb yb hb spb dt (3 unused);
+ * out[n][8] = polygon form (inter, will, tx, ty), closed form (inter, will, tx, ty). */
+int hwyo_sat_compare(const float* in, int n, float* out) {
+  for (int i = 0; i < n; ++i) {
+    const float* p = in + 12 * i;
+    Veh a = {0}, b = {0};
+    a.x = p[0], a.y = p[1], a.heading = p[2], a.speed = p[3];
+    b.x = p[4], b.y = p[5], b.heading = p[6], b.speed = p[7];
+    const float dt = p[8];
+    float A[5][2], B[5][2];
+    polygon(&a, A);
+    polygon(&b, B);
+    const float ca = hm_cosf(a.heading), sa = hm_sinf(a.heading);
+    const float cb = hm_cosf(b.heading), sb = hm_sinf(b.heading);
+    const float dax = (a.speed * ca) * dt, day = (a.speed * sa) * dt;
+    const float dbx = (b.speed * cb) * dt, dby = (b.speed * sb) * dt;
+    int i1, w1, i2, w2;
+    float* o = out + 8 * i;
+    are_polygons_intersecting(A, B, dax, day, dbx, dby, &i1, &w1, &o[2], &o[3]);
+    rect_sat(a.x, a.y, ca, sa, dax, day, b.x, b.y, cb, sb, dbx, dby, &i2, &w2, &o[6], &o[7]);
+    o[0] = (float)i1, o[1] = (float)w1, o[4] = (float)i2, o[5] = (float)w2;
+  }
+  return 0;
+}
+
 /* RoadObject.handle_collisions(other, dt) with self = road.vehicles[i], other = [j], i < j */
 static void handle_collisions(Road* r, int i, int j) {
   Veh* a = &r->v[i];
@@ -435,14 +532,13 @@ static void handle_collisions(Road* r, int i, int j) {
   float dt = r->dt;
   float dx = b->x - a->x, dy = b->y - a->y;
   if (sqrtf(dx * dx + dy * dy) > (VEH_DIAGONAL + VEH_DIAGONAL) / 2.0f + a->speed * dt) return;
-  float A[5][2], B[5][2];
-  polygon(a, A);
-  polygon(b, B);
-  float dax = (a->speed * hm_cosf(a->heading)) * dt, day = (a->speed * hm_sinf(a->heading)) * dt;
-  float dbx = (b->speed * hm_cosf(b->heading)) * dt, dby = (b->speed * hm_sinf(b->heading)) * dt;
+  const float ca = hm_cosf(a->heading), sa = hm_sinf(a->heading);
+  const float cb = hm_cosf(b->heading), sb = hm_sinf(b->heading);
+  float dax = (a->speed * ca) * dt, day = (a->speed * sa) * dt;
+  float dbx = (b->speed * cb) * dt, dby = (b->speed * sb) * dt;
   int inter, will;
   float tx, ty;
-  are_polygons_intersecting(A, B, dax, day, dbx, dby, &inter, &will, &tx, &ty);
+  rect_sat(a->x, a->y, ca, sa, dax, day, b->x, b->y, cb, sb, dbx, dby, &inter, &will, &tx, &ty);
   if (will) {
     a->imp_x = tx / 2.0f;
     a->imp_y = ty / 2.0f;
@@ -804,6 +900,9 @@ int hwyo_math(int op, const float* in, const float* in2, float* out, int n) {
       case 9: r = sqrtf(x); break;
       case 10: r = x / y; break;
       case 11: r = hm_floorf(x); break;
+      case 12: { float c_; hm_sincosf(x, &r, &c_); } break;
+      case 13: { float s_; hm_sincosf(x, &s_, &r); } break;
+      case 14: r = hm_tanf_sc(x); break;
       default: return -1;
     }
     out[i] = r;

@@ -68,6 +68,7 @@ def lib():
         L.hwyo_math.argtypes = [ctypes.c_int, _f32p, vp, _f32p, ctypes.c_int]
         L.hwyo_philox.argtypes = [_u32p, _u32p, _u32p]
         L.hwyo_philox.restype = None
+        L.hwyo_sat_compare.argtypes = [_f32p, ctypes.c_int, _f32p]
         _lib = L
     return _lib
 
@@ -153,6 +154,15 @@ def math_op(op: int, x: np.ndarray, y: Optional[np.ndarray] = None) -> np.ndarra
     yy = None if y is None else np.ascontiguousarray(y, np.float32)
     rc = lib().hwyo_math(op, x, _ptr(yy), out, x.size)
     assert rc == 0
+    return out
+
+
+def sat_compare(pairs: np.ndarray) -> np.ndarray:
+    """[n, 12] pairs (xa ya ha spa xb yb hb spb dt . . .) -> [n, 8]: upstream's polygon SAT
+    (inter, will, tx, ty) and the closed-form rectangle SAT the simulation uses."""
+    p = np.ascontiguousarray(pairs, np.float32)
+    out = np.zeros((p.shape[0], 8), np.float32)
+    assert lib().hwyo_sat_compare(p, p.shape[0], out) == 0
     return out
 
 

@@ -13,7 +13,7 @@ DEV = torch.device("cuda", 0)
 
 
 def _inputs(op, rng, n=200000):
-    if op in (0, 1, 2, 8, 11):
+    if op in (0, 1, 2, 8, 11, 12, 13, 14):
         x = np.concatenate([rng.uniform(-4, 4, n // 2), rng.uniform(-2000, 2000, n // 2)])
     elif op == 3:
         x = np.concatenate([rng.uniform(-3, 3, n // 2), rng.normal(0, 1e3, n // 2)])
@@ -35,7 +35,7 @@ def _inputs(op, rng, n=200000):
     return x.astype(np.float32), None if y is None else y.astype(np.float32)
 
 
-@pytest.mark.parametrize("op", list(range(12)))
+@pytest.mark.parametrize("op", list(range(15)))
 def test_math_library_bit_exact(op):
     rng = np.random.default_rng(op)
     x, y = _inputs(op, rng)

@@ -6,6 +6,7 @@ tests pin the restatement to closed forms and to the invariants upstream guarant
 import numpy as np
 
 from hwy import _abi
+from oracle import oracle
 from oracle.oracle import OracleEnv
 from parity_util import make_cfg
 
@@ -135,3 +136,34 @@ def test_lane_changes_and_collisions_occur_in_traffic():
         crashes += te.sum()
         changed += (env.field(_abi.F_LANE)[:, 1:V] != env.field(_abi.F_TLANE)[:, 1:V]).sum()
     assert changed > 0 and crashes > 0
+
+
+def test_rectangle_sat_closed_form_matches_polygon_sat():
+    """The closed-form rectangle SAT (oracle rect_sat, mirrored by the kernel's sat_collide)
+    against the transliteration of utils.are_polygons_intersecting on the corner polygons, over
+    vehicle pairs close enough to pass the centre-distance pre-check."""
+    rng = np.random.default_rng(11)
+    n = 200000
+    p = np.zeros((n, 12), np.float32)
+    p[:, 0] = rng.uniform(0, 500, n)
+    p[:, 1] = rng.uniform(-2, 14, n)
+    p[:, 2] = rng.normal(0, 0.3, n)
+    p[:, 3] = rng.uniform(-5, 40, n)
+    p[:, 4] = p[:, 0] + rng.uniform(-8, 8, n)
+    p[:, 5] = p[:, 1] + rng.uniform(-5, 5, n)
+    p[:, 6] = rng.normal(0, 0.3, n)
+    p[:, 7] = rng.uniform(-5, 40, n)
+    p[:, 8] = 1.0 / 15.0
+    o = oracle.sat_compare(p)
+    inter_p, will_p, inter_c, will_c = o[:, 0], o[:, 1], o[:, 4], o[:, 5]
+    # both outcomes occur often in this sample
+    assert 0.05 < inter_p.mean() < 0.95 and 0.05 < will_p.mean() < 0.95
+    # decisions agree except on rounding-level borderline pairs
+    assert np.sum(inter_p != inter_c) <= 3 and np.sum(will_p != will_c) <= 3
+    # translations: binary32 noise of coordinates ~300 m (ulp 3e-5) on both sides; where two
+    # axes tie in |distance| to that noise the two forms may pick different (near-parallel) axes
+    both = (will_p == 1) & (will_c == 1)
+    d = np.linalg.norm(o[both, 6:8] - o[both, 2:4], axis=1)
+    mag = np.linalg.norm(o[both, 2:4], axis=1)
+    assert np.mean(d <= 2e-4) > 0.999
+    assert np.all(d <= 3e-4 + 5e-3 * mag)
