@@ -17,15 +17,49 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "hwy_ppo.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// Development build only (make prof): shader-clock totals per phase of ppo_rows / ppo_wgrad,
+// summed over workgroups (wave 0), read back with hwy_ppo_debug_sections().
+#ifdef HWY_SECTION_PROFILE
+__device__ unsigned long long g_ppo_sections[16];
+#define PSEC_DECL                                \
+  uint64_t _pt = __builtin_amdgcn_s_memtime();   \
+  uint64_t _pacc[16];                            \
+  for (int _i = 0; _i < 16; ++_i) _pacc[_i] = 0;
+#define PSEC(id)                                       \
+  do {                                                 \
+    const uint64_t _n = __builtin_amdgcn_s_memtime();  \
+    _pacc[id] += _n - _pt;                             \
+    _pt = _n;                                          \
+  } while (0)
+#define PSEC_FLUSH                                                             \
+  do {                                                                         \
+    if (threadIdx.x == 0)                                                      \
+      for (int _i = 0; _i < 16; ++_i)                                          \
+        if (_pacc[_i]) atomicAdd(&g_ppo_sections[_i], _pacc[_i]);              \
+  } while (0)
+#else
+#define PSEC_DECL
+#define PSEC(id) \
+  do {           \
+  } while (0)
+#define PSEC_FLUSH \
+  do {             \
+  } while (0)
+#endif
 
 namespace {
 
 constexpr int kTile = 64;
 constexpr int kKStep = 32;
 constexpr int kHeadRows = 16;  // minibatch rows per head workgroup (4 per wave)
+constexpr int kRowTile = 16;   // minibatch rows per ppo_rows workgroup
+constexpr int kMaxRowS = 256;  // states dim bound of the fused path (LDS)
 
 struct GemmArgs {
   int M, N, K;
@@ -323,13 +357,23 @@ inline int chunk_for(int K, int split) {
 
 struct Work {
   float *h1, *h2, *ac, *dac, *dh2, *dh1;
-  float *head_part;   // [nhead][HP]
-  float *slab_ac, *bias_ac;  // [sa][2H][H], [sa][2H]
+  float *head_part;   // [max(nhead, 4 * n1)][HP]
+  float *slab_ac, *bias_ac;  // [sa][2H][H], [sa][2H]   (split-K path only)
   float *slab_2, *bias_2;    // [s2][H][H], [s2][H]
   float *slab_1, *bias_1;    // [s1][H][S], [s1][H]
-  float *norm_part;          // [nred]
+  float *norm_part;          // [max(nred, nred2)]
+  float *wg_slab;            // fused: [ntile][split][64*64 + 64] partial tiles
+  float *xg;                 // fused: [B][S] gathered states
   int nhead, HP, sa, s2, s1, ca, c2, c1, nred;
+  // fused path (ppo_rows + ppo_wgrad)
+  bool fused;
+  int n1, tac, t2, t1, nh, split, grid2, nred2;
 };
+
+// the fused row path covers the reference's shapes: float4 state rows, H a multiple of 64
+inline bool fused_ok(const hwy_ppo_dims& d) {
+  return d.S % 4 == 0 && d.S <= kMaxRowS && d.H % 64 == 0 && d.H >= 64 && d.H <= 512;
+}
 
 inline int head_stride(int H) { return 3 * H + 16; }
 constexpr int kRedThreads = 256;
@@ -353,16 +397,34 @@ inline Work carve(const hwy_ppo_dims& d, void* ws, int64_t* bytes_out) {
   w.s1 = (B + w.c1 - 1) / w.c1;
   const Layout L = make_layout(d);
   w.nred = (int)((L.numel + kRedThreads - 1) / kRedThreads);
-  int64_t sizes[14] = {
+  w.fused = fused_ok(d);
+  w.n1 = (B + kRowTile - 1) / kRowTile;
+  w.tac = (2 * H / 64) * (H / 64);
+  w.t2 = (H / 64) * (H / 64);
+  w.t1 = (H / 64) * ((S + 63) / 64);
+  w.nh = (3 * H + 9 + 63) / 64;
+  const int ntile = w.tac + w.t2 + w.t1;
+  // enough row splits to put ~256 workgroups on the chip, at least one 64-row chunk each
+  w.split = std::max(1, std::min({8, 512 / ntile, (B + 63) / 64}));  // ~2 workgroups per CU
+  w.grid2 = ntile * w.split + w.nh;
+  w.nred2 = w.nh + 4 * ntile;
+  const int64_t head_rows = w.fused ? std::max<int64_t>(w.nhead, w.n1) : w.nhead;
+  const int64_t norm_n = w.fused ? std::max(w.nred, w.nred2) : w.nred;
+  // the fused path needs no split-K slabs of full weight size, only the per-split tiles
+  const int64_t sa = w.fused ? 0 : w.sa, s2 = w.fused ? 0 : w.s2, s1 = w.fused ? 0 : w.s1;
+  const int64_t wg_slab_n = w.fused ? (int64_t)ntile * w.split * (64 * 64 + 64) : 0;
+  const int64_t xg_n = w.fused ? (int64_t)B * S : 0;
+  int64_t sizes[16] = {
       (int64_t)B * H, (int64_t)B * H, (int64_t)B * 2 * H, (int64_t)B * 2 * H, (int64_t)B * H,
-      (int64_t)B * H, (int64_t)w.nhead * w.HP, (int64_t)w.sa * 2 * H * H, (int64_t)w.sa * 2 * H,
-      (int64_t)w.s2 * H * H, (int64_t)w.s2 * H, (int64_t)w.s1 * H * S, (int64_t)w.s1 * H,
-      (int64_t)w.nred};
+      (int64_t)B * H, head_rows * w.HP, sa * 2 * H * H, sa * 2 * H,
+      s2 * H * H, s2 * H, s1 * H * S, s1 * H,
+      norm_n, wg_slab_n, xg_n};
   float* p = (float*)ws;
-  float** dst[14] = {&w.h1, &w.h2, &w.ac, &w.dac, &w.dh2, &w.dh1, &w.head_part, &w.slab_ac,
-                     &w.bias_ac, &w.slab_2, &w.bias_2, &w.slab_1, &w.bias_1, &w.norm_part};
+  float** dst[16] = {&w.h1, &w.h2, &w.ac, &w.dac, &w.dh2, &w.dh1, &w.head_part, &w.slab_ac,
+                     &w.bias_ac, &w.slab_2, &w.bias_2, &w.slab_1, &w.bias_1, &w.norm_part,
+                     &w.wg_slab, &w.xg};
   int64_t total = 0;
-  for (int i = 0; i < 14; ++i) {
+  for (int i = 0; i < 16; ++i) {
     int64_t n = (sizes[i] + 63) / 64 * 64;  // 256-B aligned sub-buffers
     if (p) *dst[i] = p + total;
     total += n;
@@ -511,6 +573,573 @@ __global__ void __launch_bounds__(256) ppo_head(HeadArgs h) {
     h.counters[0] += 1;  // Adam step t for this minibatch
     h.counters[1] += 1;  // metrics row (this step writes row counters[1]-1)
   }
+}
+
+// ----------------------------------------------------------------------------- fused row kernel
+// ppo_rows: one workgroup per 16 minibatch rows runs the whole row-local part of the step --
+// forward (3 layers), the loss head and the backward data gradients (dh2, dh1) -- with the
+// activations of its rows in LDS.  The weights stream from L2 (every workgroup reads them once
+// per layer; 1-2 MB per step, L2-resident).  v_mfma_f32_16x16x4_f32: C[16 rows][16 cols] per
+// accumulator, wave w owns output columns [w*N/4, (w+1)*N/4); A (activations) from LDS with
+// ds_read_b128, B (weights) from global -- float4 along k for [N][K] weights (forward), one
+// float per k for [K][N] weights (backward); within each 16-deep k block, sub-step j of lane
+// group g = lane>>4 uses k = kb + 4g + j (a permutation of the block the sum does not see).
+// Outputs for ppo_wgrad: h1, h2, dac, dh2, dh1 ([B][.] row-major) and per-wave head partials.
+struct RowArgs {
+  int B, S;
+  const float* states;
+  const int64_t* idx;
+  const float* pre_tanh;
+  const float* old_logp;
+  const float* adv;
+  const float* ret;
+  const float* params;
+  int64_t off[13];
+  float *h1, *h2, *dac, *dh2, *dh1;
+  float* xg;         // [B][S] gathered states (ppo_wgrad's dW1 operand)
+  float* head_part;  // [gridDim.x][HP]
+  int HP;
+  float eps_clip, value_coef, entropy_coef;
+  int32_t* counters;
+};
+
+__device__ __forceinline__ int row_pitch(int n) { return n + 4; }  // n/4 + 1 odd: conflict-free
+
+template <int QH, bool NN>
+__device__ __forceinline__ void row_gemm(const float* act, int pa, int Kp, int K, const float* W,
+                                         int ldw, int n_base, f32x4 (&acc)[QH]) {
+  constexpr int D = QH <= 4 ? 4 : 2;  // 16-deep k blocks of weights in flight
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+#pragma unroll
+  for (int t = 0; t < QH; ++t) acc[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  f32x4 wbuf[D][QH];
+  auto load = [&](int kb, f32x4(&dst)[QH]) {
+    const int k = kb + 4 * g;
+#pragma unroll
+    for (int t = 0; t < QH; ++t) {
+      const int n = n_base + 16 * t + c;
+      if (k >= K) {
+        dst[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      } else if (!NN) {
+        dst[t] = *reinterpret_cast<const f32x4*>(W + (long)n * ldw + k);
+      } else {
+        const float* p = W + (long)k * ldw + n;
+        dst[t] = f32x4{p[0], p[ldw], p[2 * ldw], p[3 * ldw]};
+      }
+    }
+  };
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (16 * d < Kp) load(16 * d, wbuf[d]);
+  for (int kb0 = 0; kb0 < Kp; kb0 += 16 * D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int kb = kb0 + 16 * d;
+      if (kb < Kp) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(act + c * pa + kb + 4 * g);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int t = 0; t < QH; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], wbuf[d][t][j], acc[t], 0, 0, 0);
+        if (kb + 16 * D < Kp) load(kb + 16 * D, wbuf[d]);
+      }
+    }
+  }
+}
+
+// C element (t, r) of lane: row 4*(lane>>4) + r, column n_base + 16 t + (lane & 15)
+template <int QH>
+__device__ __forceinline__ void row_epi_bias_relu(const f32x4 (&acc)[QH], const float* bias,
+                                                  float* out, int po, float* gout, int ldg,
+                                                  int nrows, int n_base) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+#pragma unroll
+  for (int t = 0; t < QH; ++t) {
+    const int n = n_base + 16 * t + c;
+    const float bn = bias[n];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 4 * g + r;
+      float v = acc[t][r] + bn;
+      v = v > 0.0f ? v : 0.0f;
+      out[row * po + n] = v;
+      if (gout && row < nrows) gout[(long)row * ldg + n] = v;
+    }
+  }
+}
+
+template <int QH>
+__device__ __forceinline__ void row_epi_mask(const f32x4 (&acc)[QH], float* mask_inout, int pm,
+                                             bool write_lds, float* gout, int ldg, int nrows,
+                                             int n_base) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+#pragma unroll
+  for (int t = 0; t < QH; ++t) {
+    const int n = n_base + 16 * t + c;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 4 * g + r;
+      const float v = mask_inout[row * pm + n] > 0.0f ? acc[t][r] : 0.0f;
+      if (write_lds) mask_inout[row * pm + n] = v;
+      if (row < nrows) gout[(long)row * ldg + n] = v;
+    }
+  }
+}
+
+template <int QH, int NW>
+__global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
+  constexpr int H = 64 * QH;
+  constexpr int TW = H / NW / 16;        // 16-column output tiles per wave
+  constexpr int RPW = kRowTile / NW;     // loss-head rows per wave
+  constexpr int NT = 64 * NW;            // threads
+  constexpr int WPS = 3 * H + 16;        // per-wave head-partial stride (LDS)
+  static_assert(TW * 16 * NW == H, "H must split into 16-column tiles per wave");
+  constexpr int PH = H + 4, PA = 2 * H + 4, PXMAX = kMaxRowS + 4;
+  static_assert(NW * WPS <= kRowTile * PA, "head partials must fit the [a1|c1] image");
+  __shared__ __attribute__((aligned(16))) float X[kRowTile * PXMAX];
+  __shared__ __attribute__((aligned(16))) float H1[kRowTile * PH];
+  __shared__ __attribute__((aligned(16))) float H2[kRowTile * PH];
+  __shared__ __attribute__((aligned(16))) float AC[kRowTile * PA];
+  PSEC_DECL
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int S = r.S, Sp = (S + 15) / 16 * 16, px = row_pitch(Sp);
+  const int row0 = blockIdx.x * kRowTile;
+  const int nrows = min(kRowTile, r.B - row0);
+  const float* P = r.params;
+  // gathered states rows, zero-padded to Sp columns and 16 rows
+  for (int e = t; e < kRowTile * (Sp / 4); e += NT) {
+    const int row = e / (Sp / 4), k = 4 * (e % (Sp / 4));
+    f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (row < nrows && k < S) {
+      v = *reinterpret_cast<const f32x4*>(r.states + r.idx[row0 + row] * (long)S + k);
+      *reinterpret_cast<f32x4*>(r.xg + (long)(row0 + row) * S + k) = v;
+    }
+    *reinterpret_cast<f32x4*>(&X[row * px + k]) = v;
+  }
+  __syncthreads();
+  PSEC(0);
+  const int nb = w * (H / NW);  // this wave's output columns of an H-wide layer
+  f32x4 acc[TW];
+  // h1 = relu(x W1^T + b1)
+  row_gemm<TW, false>(X, px, Sp, S, P + r.off[P_W1], S, nb, acc);
+  row_epi_bias_relu<TW>(acc, P + r.off[P_B1], H1, PH, r.h1 + (long)row0 * H, H, nrows, nb);
+  __syncthreads();
+  PSEC(1);
+  // h2 = relu(h1 W2^T + b2)
+  row_gemm<TW, false>(H1, PH, H, H, P + r.off[P_W2], H, nb, acc);
+  row_epi_bias_relu<TW>(acc, P + r.off[P_B2], H2, PH, r.h2 + (long)row0 * H, H, nrows, nb);
+  __syncthreads();
+  PSEC(2);
+  // [a1 | c1] = relu(h2 [Wa1; Wc1]^T + [ba1; bc1])
+  row_gemm<TW, false>(H2, PH, H, H, P + r.off[P_WA1], H, nb, acc);
+  row_epi_bias_relu<TW>(acc, P + r.off[P_BA1], AC, PA, nullptr, 0, nrows, nb);
+  row_gemm<TW, false>(H2, PH, H, H, P + r.off[P_WC1], H, nb, acc);
+  row_epi_bias_relu<TW>(acc, P + r.off[P_BC1], AC + H, PA, nullptr, 0, nrows, nb);
+  __syncthreads();
+  PSEC(3);
+
+  // ---- loss head (ppo/agent.py:226-245): wave w takes rows RPW*w ..; lane owns the hidden
+  // columns lane + 64q; dL/d[a1|c1] overwrites [a1|c1] in LDS (and goes to HBM for ppo_wgrad);
+  // the head weight / bias / log_std gradients stay in registers until the waves combine them
+  float ga0[QH], ga1[QH], gc[QH];
+  float s_dba0 = 0, s_dba1 = 0, s_dbc = 0, s_dls0 = 0, s_dls1 = 0;
+  float s_pg = 0, s_vf = 0, s_clip = 0, s_kl = 0;
+  {
+    float wa0[QH], wa1[QH], wc[QH];
+#pragma unroll
+    for (int q = 0; q < QH; ++q) {
+      const int col = lane + 64 * q;
+      wa0[q] = P[r.off[P_WA2] + col];
+      wa1[q] = P[r.off[P_WA2] + H + col];
+      wc[q] = P[r.off[P_WC2] + col];
+      ga0[q] = ga1[q] = gc[q] = 0.0f;
+    }
+    const float ba0 = P[r.off[P_BA2]], ba1 = P[r.off[P_BA2] + 1], bcv = P[r.off[P_BC2]];
+    const float ls0 = P[r.off[P_LOGSTD]], ls1 = P[r.off[P_LOGSTD] + 1];
+    // torch Normal: scale = exp(log_std); var = scale**2; log_scale = log(scale)
+    const float sc0 = expf(ls0), sc1 = expf(ls1);
+    const float var0 = sc0 * sc0, var1 = sc1 * sc1;
+    const float lsc0 = logf(sc0), lsc1 = logf(sc1);
+    const float LOG_SQRT_2PI = 0.91893853320467274178f;
+    const float invB = 1.0f / (float)r.B;
+    const float lo = 1.0f - r.eps_clip, hi = 1.0f + r.eps_clip;
+    for (int rr = 0; rr < RPW; ++rr) {
+      const int lr = RPW * w + rr;
+      if (lr >= nrows) break;
+      const int b = row0 + lr;
+      float* arow = AC + lr * PA;
+      float a[QH], cc[QH];
+      float p0 = 0.0f, p1 = 0.0f, pv = 0.0f;
+#pragma unroll
+      for (int q = 0; q < QH; ++q) {
+        const int col = lane + 64 * q;
+        a[q] = arow[col];
+        cc[q] = arow[H + col];
+        p0 += a[q] * wa0[q];
+        p1 += a[q] * wa1[q];
+        pv += cc[q] * wc[q];
+      }
+      const long src = (long)r.idx[b];
+      const float z0 = r.pre_tanh[src * 2], z1 = r.pre_tanh[src * 2 + 1];
+      const float old = r.old_logp[src], ad = r.adv[src], rt = r.ret[src];
+      const float mu0 = wave_sum(p0) + ba0, mu1 = wave_sum(p1) + ba1, val = wave_sum(pv) + bcv;
+      const float d0 = z0 - mu0, d1 = z1 - mu1;
+      const float t0 = tanhf(z0), t1 = tanhf(z1);
+      const float lp0 = -(d0 * d0) / (2.0f * var0) - lsc0 - LOG_SQRT_2PI;
+      const float lp1 = -(d1 * d1) / (2.0f * var1) - lsc1 - LOG_SQRT_2PI;
+      const float logp =
+          (lp0 - log1pf(-(t0 * t0) + 1e-6f)) + (lp1 - log1pf(-(t1 * t1) + 1e-6f));
+      const float log_ratio = logp - old;
+      const float ratio = expf(log_ratio);
+      const float cr = fminf(fmaxf(ratio, lo), hi);
+      const float s1 = ratio * ad, s2 = cr * ad;
+      const float inr = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
+      // torch.min / clamp backward: ties split the gradient evenly
+      const float wsel = s1 < s2 ? 1.0f : (s1 > s2 ? inr : 0.5f * (1.0f + inr));
+      const float dlogp = -invB * ad * wsel * ratio;  // d(actor_loss)/d(logp)
+      const float dmu0 = dlogp * d0 / var0, dmu1 = dlogp * d1 / var1;
+      const float dv = r.value_coef * 2.0f * (val - rt) * invB;
+      float* grow = r.dac + (long)b * 2 * H;
+#pragma unroll
+      for (int q = 0; q < QH; ++q) {
+        const int col = lane + 64 * q;
+        const float da = a[q] > 0.0f ? (dmu0 * wa0[q] + dmu1 * wa1[q]) : 0.0f;
+        const float dc = cc[q] > 0.0f ? dv * wc[q] : 0.0f;
+        arow[col] = da;
+        arow[H + col] = dc;
+        grow[col] = da;
+        grow[H + col] = dc;
+        ga0[q] += dmu0 * a[q];
+        ga1[q] += dmu1 * a[q];
+        gc[q] += dv * cc[q];
+      }
+      s_dba0 += dmu0;
+      s_dba1 += dmu1;
+      s_dbc += dv;
+      s_dls0 += dlogp * ((d0 * d0) / var0 - 1.0f);
+      s_dls1 += dlogp * ((d1 * d1) / var1 - 1.0f);
+      s_pg += -fminf(s1, s2);
+      s_vf += (val - rt) * (val - rt);
+      s_clip += fabsf(ratio - 1.0f) > r.eps_clip ? 1.0f : 0.0f;
+      s_kl += (ratio - 1.0f) - log_ratio;
+    }
+    if (blockIdx.x == 0 && t == 0) {
+      r.counters[0] += 1;  // Adam step t for this minibatch
+      r.counters[1] += 1;  // metrics row (this step writes row counters[1]-1)
+    }
+  }
+  __syncthreads();
+  PSEC(4);
+  // dh2 = (dac [Wa1; Wc1]) * (h2 > 0)   ([Wa1; Wc1] is [2H][H]: k-major); the two halves of
+  // K = 2H (Wa1 rows, Wc1 rows) are summed at the end
+  {
+    f32x4 acc2[TW];
+    row_gemm<TW, true>(AC, PA, H, H, P + r.off[P_WA1], H, nb, acc);
+    row_gemm<TW, true>(AC + H, PA, H, H, P + r.off[P_WC1], H, nb, acc2);
+#pragma unroll
+    for (int q = 0; q < TW; ++q) acc[q] = acc[q] + acc2[q];
+  }
+  row_epi_mask<TW>(acc, H2, PH, true, r.dh2 + (long)row0 * H, H, nrows, nb);
+  __syncthreads();
+  PSEC(5);
+  // the head partials of the NW waves -> one row per workgroup (fixed order); [a1|c1] is free
+  {
+    float* wp = AC + w * WPS;
+#pragma unroll
+    for (int q = 0; q < QH; ++q) {
+      const int col = lane + 64 * q;
+      wp[col] = ga0[q];
+      wp[H + col] = ga1[q];
+      wp[2 * H + col] = gc[q];
+    }
+    if (lane == 0) {
+      float* tl = wp + 3 * H;
+      tl[0] = s_dba0, tl[1] = s_dba1, tl[2] = s_dbc, tl[3] = s_dls0, tl[4] = s_dls1;
+      tl[5] = s_pg, tl[6] = s_vf, tl[7] = s_clip, tl[8] = s_kl;
+    }
+    __syncthreads();
+    float* out = r.head_part + (long)blockIdx.x * r.HP;
+    for (int j = t; j < 3 * H + 9; j += NT) {
+      float v = AC[j];
+#pragma unroll
+      for (int ww = 1; ww < NW; ++ww) v += AC[ww * WPS + j];
+      out[j] = v;
+    }
+  }
+  // dh1 = (dh2 W2) * (h1 > 0)
+  row_gemm<TW, true>(H2, PH, H, H, P + r.off[P_W2], H, nb, acc);
+  row_epi_mask<TW>(acc, H1, PH, false, r.dh1 + (long)row0 * H, H, nrows, nb);
+  PSEC(6);
+  PSEC_FLUSH;
+}
+
+// ----------------------------------------------------------------------------- weight grads
+// ppo_wgrad: every weight gradient as a full-K (= minibatch) 32x32 tile -- no split-K slabs --
+// plus the bias column sums, the head-parameter sums over the ppo_rows partials, the metrics
+// row and one sum-of-squares partial per workgroup for clip_grad_norm_.  Tiles: dWac = dac^T h2
+// (rows < H -> Wa1, >= H -> Wc1), dW2 = dh2^T h1, dW1 = dh1^T gather(states); 4 waves split the
+// minibatch rows and their tiles are summed in a fixed order (deterministic).
+struct WgArgs {
+  int B, S, H;
+  const float *dac, *h2, *dh2, *h1, *dh1, *xg;
+  float* grads;
+  int64_t off[13];
+  const float* head_part;
+  int nhp, HP;
+  float* norm_part;
+  int tac, t2, t1, nh;  // 64x64 tiles per region, head-sum workgroups
+  int split;            // minibatch-row splits per tile (workgroups per tile)
+  float* slab;          // [tiles][split][64*64 + 64] partial tiles + bias partials
+  float entropy_coef, value_coef, ent_const;
+  const float* params;
+  float* metrics;
+  int32_t* counters;
+};
+
+__device__ __forceinline__ float block_sum4(float v, float* red) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  __syncthreads();
+  if ((t & 63) == 0) red[t >> 6] = v;
+  __syncthreads();
+  return ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+// LDS image of a 64-row chunk: row k, column col at k*64 + (col ^ 32*(k&1)), so the two lane
+// halves of an MFMA operand read (rows 2s, 2s+1) hit disjoint banks
+__device__ __forceinline__ int wg_sw(int k, int col) { return k * 64 + (col ^ ((k & 1) << 5)); }
+
+__global__ void __launch_bounds__(256) ppo_wgrad(WgArgs a) {
+  PSEC_DECL
+  __shared__ __attribute__((aligned(16))) float wg_lds[4 * 64 * 64];
+  __shared__ float red[4];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, l32 = lane & 31;
+  const int H = a.H;
+  const int ntile = a.tac + a.t2 + a.t1;
+  int id = blockIdx.x;
+  float sq = 0.0f;
+  if (id >= ntile * a.split) {  // ---- head parameters + metrics
+    float(*tile)[64] = reinterpret_cast<float(*)[64]>(wg_lds);
+    const int hid = id - ntile * a.split;
+    const int e = hid * 64 + lane;
+    const int ne = 3 * H + 9;
+    const int per = (a.nhp + 3) / 4, p0 = w * per, p1 = min(a.nhp, p0 + per);
+    float s = 0.0f;
+    if (e < ne) {
+      for (int pb = p0; pb < p1; pb += 16) {  // 16 loads in flight, summed in row order
+        float pv[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          pv[u] = pb + u < p1 ? a.head_part[(long)(pb + u) * a.HP + e] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s += pv[u];
+      }
+    }
+    tile[w][lane] = s;
+    __syncthreads();
+    float g = 0.0f;
+    if (t < 64 && e < ne) {
+      g = ((tile[0][t] + tile[1][t]) + tile[2][t]) + tile[3][t];
+      long dst = -1;
+      float gv = g;
+      if (e < 2 * H) {
+        dst = a.off[P_WA2] + e;
+      } else if (e < 3 * H) {
+        dst = a.off[P_WC2] + (e - 2 * H);
+      } else {
+        const int k = e - 3 * H;
+        if (k < 2) dst = a.off[P_BA2] + k;
+        else if (k == 2) dst = a.off[P_BC2];
+        else if (k < 5) dst = a.off[P_LOGSTD] + (k - 3), gv = g - a.entropy_coef;
+      }
+      if (dst >= 0) {
+        a.grads[dst] = gv;
+        sq = gv * gv;
+      }
+      tile[0][t] = g;  // keep the totals for the metrics row
+    }
+    const float tot = block_sum4(sq, red);
+    if (t == 0) a.norm_part[hid] = tot;
+    if (3 * H >= e - lane && 3 * H < e - lane + 64 && t == 0) {
+      // metrics row (ppo/agent.py:255-262): policy, value, entropy, loss, clip count, kl
+      const int k0 = 3 * H - (e - lane);
+      const float pg = tile[0][k0 + 5], vf = tile[0][k0 + 6], clip = tile[0][k0 + 7],
+                  kl = tile[0][k0 + 8];
+      const float invB = 1.0f / (float)a.B;
+      const float ls0 = a.params[a.off[P_LOGSTD]], ls1 = a.params[a.off[P_LOGSTD] + 1];
+      const float ent = (a.ent_const + logf(expf(ls0))) + (a.ent_const + logf(expf(ls1)));
+      float* m = a.metrics + (int64_t)(a.counters[1] - 1) * 6;
+      m[0] = pg * invB;
+      m[1] = vf * invB;
+      m[2] = ent;
+      m[3] = (pg * invB + a.value_coef * (vf * invB)) - a.entropy_coef * ent;
+      m[4] = clip;
+      m[5] = kl * invB;
+    }
+    PSEC(10);
+    PSEC_FLUSH;
+    return;
+  }
+  // ---- a 64x64 weight-gradient tile over 1/split of the minibatch rows.  z = id % split: with
+  // split = 8 every XCD (workgroup id mod 8) works on one 1/8 slice of the minibatch rows, whose
+  // activations (~3 MB at B = 4096, H = 256) stay in that XCD's L2 for all the tiles
+  const int z = id % a.split;
+  id /= a.split;
+  const int tile_id = id;
+  const float *A, *Bm;
+  int lda, ldb, N, ntj, region;
+  if (id < a.tac) {  // dWac = dac^T h2
+    A = a.dac, lda = 2 * H, Bm = a.h2, ldb = H, N = H, ntj = H / 64, region = 0;
+  } else if (id < a.tac + a.t2) {  // dW2 = dh2^T h1
+    id -= a.tac;
+    A = a.dh2, lda = H, Bm = a.h1, ldb = H, N = H, ntj = H / 64, region = 1;
+  } else {  // dW1 = dh1^T x (gathered states rows written by ppo_rows)
+    id -= a.tac + a.t2;
+    A = a.dh1, lda = H, Bm = a.xg, ldb = a.S, N = a.S, ntj = (a.S + 63) / 64, region = 2;
+  }
+  const int ti = id / ntj, tj = id % ntj;
+  const int i0 = ti * 64, j0 = tj * 64;
+  const int rows = (a.B + a.split - 1) / a.split;
+  const int kb0 = z * rows, kb1 = min(a.B, kb0 + rows);
+  // K-chunks of 64 rows: A[64][64] and B[64][64] images (pitch 64) double-buffered in LDS,
+  // the next chunk's float4s in registers while the current one feeds the MFMAs
+  float* As0 = wg_lds;
+  float* Bs0 = wg_lds + 64 * 64;
+  float* As1 = wg_lds + 2 * 64 * 64;
+  float* Bs1 = wg_lds + 3 * 64 * 64;
+  // The next two chunks' float4s stay in flight in two register sets while one chunk feeds the
+  // MFMAs from LDS (double-buffered images).  Loads are unconditional (rows past the split and
+  // columns past N are clamped into range and zeroed when stashed), so the waits are counted.
+  auto fetch = [&](int k0, f32x4(&ra)[4], f32x4(&rb)[4]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e4 = t + 256 * q, rr = e4 >> 4, c4 = (e4 & 15) * 4;
+      const int kk = min(k0 + rr, kb1 - 1);
+      const int cb = min(j0 + c4, N - 4);
+      ra[q] = *reinterpret_cast<const f32x4*>(A + (long)kk * lda + i0 + c4);
+      rb[q] = *reinterpret_cast<const f32x4*>(Bm + (long)kk * ldb + cb);
+    }
+  };
+  auto stash = [&](float* As, float* Bs, const f32x4(&ra)[4], const f32x4(&rb)[4], int k0) {
+    const f32x4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e4 = t + 256 * q, rr = e4 >> 4, c4 = (e4 & 15) * 4;
+      const bool rok = k0 + rr < kb1;
+      *reinterpret_cast<f32x4*>(&As[wg_sw(rr, c4)]) = rok ? ra[q] : zero;
+      *reinterpret_cast<f32x4*>(&Bs[wg_sw(rr, c4)]) = (rok && j0 + c4 < N) ? rb[q] : zero;
+    }
+  };
+  const int wm = (w & 1) * 32, wn = (w >> 1) * 32;
+  f32x16 acc;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+  float bsum = 0.0f;  // column sums of A (bias gradient), threads 0..63, tiles with tj == 0
+  const bool do_bias = tj == 0 && t < 64;
+  auto compute = [&](const float* As, const float* Bs) {
+#pragma unroll 8
+    for (int s = 0; s < 32; ++s) {
+      const int k = 2 * s + h;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[wg_sw(k, wm + l32)], Bs[wg_sw(k, wn + l32)],
+                                                 acc, 0, 0, 0);
+    }
+    if (do_bias) {
+#pragma unroll 8
+      for (int k = 0; k < 64; ++k) bsum += As[wg_sw(k, t)];
+    }
+  };
+  const int nchunk = (kb1 - kb0 + 63) / 64;  // >= 1 (split <= B / 64)
+  f32x4 ra0[4], rb0[4], ra1[4], rb1[4];
+  fetch(kb0, ra0, rb0);
+  fetch(kb0 + 64, ra1, rb1);
+  stash(As0, Bs0, ra0, rb0, kb0);
+  fetch(kb0 + 128, ra0, rb0);
+  __syncthreads();
+  for (int c = 0; c < nchunk; c += 2) {
+    // even chunk c from buffer 0; chunk c+1 (set 1) -> buffer 1; set 1 <- chunk c+3
+    stash(As1, Bs1, ra1, rb1, kb0 + 64 * (c + 1));
+    fetch(kb0 + 64 * (c + 3), ra1, rb1);
+    compute(As0, Bs0);
+    __syncthreads();
+    if (c + 1 >= nchunk) break;
+    // odd chunk c+1 from buffer 1; chunk c+2 (set 0) -> buffer 0; set 0 <- chunk c+4
+    stash(As0, Bs0, ra0, rb0, kb0 + 64 * (c + 2));
+    fetch(kb0 + 64 * (c + 4), ra0, rb0);
+    compute(As1, Bs1);
+    __syncthreads();
+  }
+  PSEC(8);
+  // partial tile (+ bias column sums) -> slab; ppo_wsum adds the splits
+  float* slab = a.slab + ((long)tile_id * a.split + z) * (64 * 64 + 64);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int ri = wm + (q & 3) + 8 * (q >> 2) + 4 * h;
+    slab[ri * 64 + wn + l32] = acc[q];
+  }
+  if (t < 64) slab[64 * 64 + t] = bsum;
+  PSEC(9);
+  PSEC_FLUSH;
+}
+
+// ppo_wsum: the `split` partial tiles of every weight-gradient tile summed in split order
+// (deterministic) into the flat gradient, one quarter tile per workgroup (4 elements x all
+// splits in flight per thread), plus the bias sums and a sum-of-squares partial each.
+__global__ void __launch_bounds__(256) ppo_wsum(WgArgs a) {
+  __shared__ float red[4];
+  const int t = threadIdx.x, H = a.H;
+  const int tile_id = blockIdx.x >> 2, quarter = blockIdx.x & 3;
+  int id = tile_id, ntj, N, region;
+  if (id < a.tac) {
+    ntj = H / 64, N = H, region = 0;
+  } else if (id < a.tac + a.t2) {
+    id -= a.tac, ntj = H / 64, N = H, region = 1;
+  } else {
+    id -= a.tac + a.t2, ntj = (a.S + 63) / 64, N = a.S, region = 2;
+  }
+  const int ti = id / ntj, tj = id % ntj, i0 = ti * 64, j0 = tj * 64;
+  long base, bbase;
+  int ldo;
+  if (region == 0) {  // dWac rows -> Wa1 / Wc1
+    base = i0 < H ? a.off[P_WA1] + (long)i0 * H : a.off[P_WC1] + (long)(i0 - H) * H;
+    bbase = i0 < H ? a.off[P_BA1] + i0 : a.off[P_BC1] + (i0 - H);
+    ldo = H;
+  } else if (region == 1) {
+    base = a.off[P_W2] + (long)i0 * H, bbase = a.off[P_B2] + i0, ldo = H;
+  } else {
+    base = a.off[P_W1] + (long)i0 * a.S, bbase = a.off[P_B1] + i0, ldo = a.S;
+  }
+  const float* sl = a.slab + (long)tile_id * a.split * (64 * 64 + 64);
+  constexpr int kMaxSplit = 8;
+  float pv[4][kMaxSplit];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int zz = 0; zz < kMaxSplit; ++zz)
+      pv[q][zz] = zz < a.split ? sl[(long)zz * (64 * 64 + 64) + quarter * 1024 + t + 256 * q]
+                               : 0.0f;
+  float sq = 0.0f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = quarter * 1024 + t + 256 * q, ri = e >> 6, cj = e & 63;
+    float v = pv[q][0];
+#pragma unroll
+    for (int zz = 1; zz < kMaxSplit; ++zz)
+      if (zz < a.split) v += pv[q][zz];
+    if (j0 + cj < N) {
+      a.grads[base + (long)ri * ldo + j0 + cj] = v;
+      sq += v * v;
+    }
+  }
+  if (quarter == 0 && tj == 0 && t < 64) {  // bias = column sum of the output-gradient matrix
+    float v = 0.0f;
+    for (int zz = 0; zz < a.split; ++zz) v += sl[(long)zz * (64 * 64 + 64) + 64 * 64 + t];
+    a.grads[bbase + t] = v;
+    sq += v * v;
+  }
+  const float tot = block_sum4(sq, red);
+  if (t == 0) a.norm_part[a.nh + blockIdx.x] = tot;
 }
 
 // ----------------------------------------------------------------------------- reduce
@@ -701,7 +1330,47 @@ int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
   Work w = carve(d, a->workspace, nullptr);
   const float* P = a->params;
   int rc = 0;
-  // ---- forward
+  if (w.fused) {
+    RowArgs r = {};
+    r.B = B, r.S = S;
+    r.states = a->states, r.idx = a->idx, r.pre_tanh = a->pre_tanh, r.old_logp = a->old_logp;
+    r.adv = a->adv, r.ret = a->ret, r.params = P;
+    for (int i = 0; i < 13; ++i) r.off[i] = L.off[i];
+    r.h1 = w.h1, r.h2 = w.h2, r.dac = w.dac, r.dh2 = w.dh2, r.dh1 = w.dh1, r.xg = w.xg;
+    r.head_part = w.head_part, r.HP = w.HP;
+    r.eps_clip = a->eps_clip, r.value_coef = a->value_coef, r.entropy_coef = a->entropy_coef;
+    r.counters = a->counters;
+    // 8 waves (2 per SIMD) when the columns split into 16-wide tiles, else 4
+    const dim3 g1(w.n1), b4(256), b8(512), blk(256);
+    switch (H / 64) {
+      case 1: hipLaunchKernelGGL((ppo_rows<1, 4>), g1, b4, 0, s, r); break;
+      case 2: hipLaunchKernelGGL((ppo_rows<2, 8>), g1, b8, 0, s, r); break;
+      case 3: hipLaunchKernelGGL((ppo_rows<3, 4>), g1, b4, 0, s, r); break;
+      case 4: hipLaunchKernelGGL((ppo_rows<4, 8>), g1, b8, 0, s, r); break;
+      case 5: hipLaunchKernelGGL((ppo_rows<5, 4>), g1, b4, 0, s, r); break;
+      case 6: hipLaunchKernelGGL((ppo_rows<6, 8>), g1, b8, 0, s, r); break;
+      case 7: hipLaunchKernelGGL((ppo_rows<7, 4>), g1, b4, 0, s, r); break;
+      default: hipLaunchKernelGGL((ppo_rows<8, 8>), g1, b8, 0, s, r); break;
+    }
+    rc |= hipGetLastError() == hipSuccess ? 0 : -1;
+    WgArgs g = {};
+    g.B = B, g.S = S, g.H = H;
+    g.dac = w.dac, g.h2 = w.h2, g.dh2 = w.dh2, g.h1 = w.h1, g.dh1 = w.dh1, g.xg = w.xg;
+    g.grads = a->grads;
+    for (int i = 0; i < 13; ++i) g.off[i] = L.off[i];
+    g.head_part = w.head_part, g.nhp = w.n1, g.HP = w.HP, g.norm_part = w.norm_part;
+    g.tac = w.tac, g.t2 = w.t2, g.t1 = w.t1, g.nh = w.nh;
+    g.split = w.split, g.slab = w.wg_slab;
+    g.entropy_coef = a->entropy_coef, g.value_coef = a->value_coef;
+    g.ent_const = 0.5f + 0.91893853320467274178f;
+    g.params = P, g.metrics = a->metrics, g.counters = a->counters;
+    hipLaunchKernelGGL(ppo_wgrad, dim3(w.grid2), blk, 0, s, g);
+    rc |= hipGetLastError() == hipSuccess ? 0 : -1;
+    hipLaunchKernelGGL(ppo_wsum, dim3(4 * (w.tac + w.t2 + w.t1)), blk, 0, s, g);
+    rc |= hipGetLastError() == hipSuccess ? 0 : -1;
+    return rc;
+  }
+  // ---- forward (general path: separate GEMMs, split-K weight gradients)
   {
     GemmArgs g = gemm_args();
     g.M = B, g.N = H, g.K = S;
@@ -830,11 +1499,25 @@ int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream) {
   }
   OptArgs o = {};
   o.params = a->params, o.grads = a->grads, o.m = a->adam_m, o.v = a->adam_v;
-  o.norm_part = w.norm_part, o.nred = w.nred, o.numel = L.numel, o.counters = a->counters;
+  // norm partials: ppo_sumsq / ppo_reduce write nred of them, ppo_wgrad grid2
+  o.norm_part = w.norm_part, o.numel = L.numel, o.counters = a->counters;
+  o.nred = (w.fused && !a->grads_modified) ? w.nred2 : w.nred;
   o.lr = a->lr, o.beta1 = a->beta1, o.beta2 = a->beta2, o.eps = a->adam_eps;
   o.max_norm = a->max_grad_norm;
   hipLaunchKernelGGL(ppo_adam, dim3(w.nred), dim3(256), 0, s, o);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+#ifdef HWY_SECTION_PROFILE
+int hwy_ppo_debug_sections(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ppo_sections), sizeof(g_ppo_sections)) != hipSuccess)
+    return -2;
+  if (reset) {
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_ppo_sections), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return 0;
+}
+#endif
 
 }  // extern "C"

@@ -105,7 +105,7 @@ class FusedPPO:
                 p.grad = self.grads[off:off + n].view_as(p)
                 self.params.append(p)
         self.offs = offs
-        self.workspace = torch.empty(int(ws), device=dev, dtype=torch.uint8)
+        self.workspace = torch.zeros(int(ws), device=dev, dtype=torch.uint8)  # counters start at 0
         self.counters = torch.zeros(2, device=dev, dtype=torch.int32)
         self.metrics = torch.zeros(max(1, agent.epochs * nmb), 6, device=dev)
         self.group = group

@@ -53,7 +53,7 @@ typedef struct hwy_ppo_args {
   float* adam_v;
   int32_t* counters;      /* [0] Adam step t, [1] metrics row */
   float* metrics;         /* [rows, 6]: policy, value, entropy, loss, clip count, kl */
-  void* workspace;
+  void* workspace;        /* hwy_ppo_workspace_bytes(dims) bytes, owned by these calls */
   /* hyper-parameters (PPOAgent defaults: eps_clip .2, value_coef .5, entropy_coef .005) */
   float eps_clip, value_coef, entropy_coef, max_grad_norm;
   float lr, beta1, beta2, adam_eps;
