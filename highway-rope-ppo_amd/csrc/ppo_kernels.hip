@@ -687,6 +687,52 @@ __device__ __forceinline__ void row_epi_mask(const f32x4 (&acc)[QH], float* mask
   }
 }
 
+// Forward of the 16 rows starting at row0 (rows idx[row0 + i], or row0 + i without idx) into
+// the LDS images X, H1, H2, AC = [a1 | c1]; optionally also to HBM (xg, h1, h2; null = no).
+// Ends with a workgroup barrier.
+template <int QH, int NW>
+__device__ __forceinline__ void rows_forward(const float* states, const int64_t* idx, int S,
+                                             int nrows, int row0, const float* P,
+                                             const int64_t* off, float* X, float* H1, float* H2,
+                                             float* AC, float* xg, float* h1g, float* h2g) {
+  constexpr int H = 64 * QH;
+  constexpr int TW = H / NW / 16;
+  constexpr int NT = 64 * NW;
+  constexpr int PH = H + 4, PA = 2 * H + 4;
+  const int t = threadIdx.x, w = t >> 6;
+  const int Sp = (S + 15) / 16 * 16, px = row_pitch(Sp);
+  // states rows, zero-padded to Sp columns and 16 rows
+  for (int e = t; e < kRowTile * (Sp / 4); e += NT) {
+    const int row = e / (Sp / 4), k = 4 * (e % (Sp / 4));
+    f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (row < nrows && k < S) {
+      const long src = idx ? (long)idx[row0 + row] : (long)(row0 + row);
+      v = *reinterpret_cast<const f32x4*>(states + src * S + k);
+      if (xg) *reinterpret_cast<f32x4*>(xg + (long)(row0 + row) * S + k) = v;
+    }
+    *reinterpret_cast<f32x4*>(&X[row * px + k]) = v;
+  }
+  __syncthreads();
+  const int nb = w * (H / NW);  // this wave's output columns of an H-wide layer
+  f32x4 acc[TW];
+  // h1 = relu(x W1^T + b1)
+  row_gemm<TW, false>(X, px, Sp, S, P + off[P_W1], S, nb, acc);
+  row_epi_bias_relu<TW>(acc, P + off[P_B1], H1, PH, h1g ? h1g + (long)row0 * H : nullptr, H,
+                        nrows, nb);
+  __syncthreads();
+  // h2 = relu(h1 W2^T + b2)
+  row_gemm<TW, false>(H1, PH, H, H, P + off[P_W2], H, nb, acc);
+  row_epi_bias_relu<TW>(acc, P + off[P_B2], H2, PH, h2g ? h2g + (long)row0 * H : nullptr, H,
+                        nrows, nb);
+  __syncthreads();
+  // [a1 | c1] = relu(h2 [Wa1; Wc1]^T + [ba1; bc1])
+  row_gemm<TW, false>(H2, PH, H, H, P + off[P_WA1], H, nb, acc);
+  row_epi_bias_relu<TW>(acc, P + off[P_BA1], AC, PA, nullptr, 0, nrows, nb);
+  row_gemm<TW, false>(H2, PH, H, H, P + off[P_WC1], H, nb, acc);
+  row_epi_bias_relu<TW>(acc, P + off[P_BC1], AC + H, PA, nullptr, 0, nrows, nb);
+  __syncthreads();
+}
+
 template <int QH, int NW>
 __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   constexpr int H = 64 * QH;
@@ -703,41 +749,15 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   __shared__ __attribute__((aligned(16))) float AC[kRowTile * PA];
   PSEC_DECL
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int S = r.S, Sp = (S + 15) / 16 * 16, px = row_pitch(Sp);
+  const int S = r.S;
   const int row0 = blockIdx.x * kRowTile;
   const int nrows = min(kRowTile, r.B - row0);
   const float* P = r.params;
-  // gathered states rows, zero-padded to Sp columns and 16 rows
-  for (int e = t; e < kRowTile * (Sp / 4); e += NT) {
-    const int row = e / (Sp / 4), k = 4 * (e % (Sp / 4));
-    f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (row < nrows && k < S) {
-      v = *reinterpret_cast<const f32x4*>(r.states + r.idx[row0 + row] * (long)S + k);
-      *reinterpret_cast<f32x4*>(r.xg + (long)(row0 + row) * S + k) = v;
-    }
-    *reinterpret_cast<f32x4*>(&X[row * px + k]) = v;
-  }
-  __syncthreads();
-  PSEC(0);
+  rows_forward<QH, NW>(r.states, r.idx, S, nrows, row0, P, r.off, X, H1, H2, AC, r.xg, r.h1,
+                       r.h2);
+  PSEC(3);
   const int nb = w * (H / NW);  // this wave's output columns of an H-wide layer
   f32x4 acc[TW];
-  // h1 = relu(x W1^T + b1)
-  row_gemm<TW, false>(X, px, Sp, S, P + r.off[P_W1], S, nb, acc);
-  row_epi_bias_relu<TW>(acc, P + r.off[P_B1], H1, PH, r.h1 + (long)row0 * H, H, nrows, nb);
-  __syncthreads();
-  PSEC(1);
-  // h2 = relu(h1 W2^T + b2)
-  row_gemm<TW, false>(H1, PH, H, H, P + r.off[P_W2], H, nb, acc);
-  row_epi_bias_relu<TW>(acc, P + r.off[P_B2], H2, PH, r.h2 + (long)row0 * H, H, nrows, nb);
-  __syncthreads();
-  PSEC(2);
-  // [a1 | c1] = relu(h2 [Wa1; Wc1]^T + [ba1; bc1])
-  row_gemm<TW, false>(H2, PH, H, H, P + r.off[P_WA1], H, nb, acc);
-  row_epi_bias_relu<TW>(acc, P + r.off[P_BA1], AC, PA, nullptr, 0, nrows, nb);
-  row_gemm<TW, false>(H2, PH, H, H, P + r.off[P_WC1], H, nb, acc);
-  row_epi_bias_relu<TW>(acc, P + r.off[P_BC1], AC + H, PA, nullptr, 0, nrows, nb);
-  __syncthreads();
-  PSEC(3);
 
   // ---- loss head (ppo/agent.py:226-245): wave w takes rows RPW*w ..; lane owns the hidden
   // columns lane + 64q; dL/d[a1|c1] overwrites [a1|c1] in LDS (and goes to HBM for ppo_wgrad);
@@ -872,6 +892,84 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   row_epi_mask<TW>(acc, H1, PH, false, r.dh1 + (long)row0 * H, H, nrows, nb);
   PSEC(6);
   PSEC_FLUSH;
+}
+
+// ----------------------------------------------------------------------------- acting
+// ppo_act: ActorCritic.act for a batch of states (ppo/agent.py act(): forward, z = mean +
+// exp(log_std) * eps, action = tanh(z), squashed Normal log-prob, value) -- the forward of
+// ppo_rows followed by a per-row sampling head; noise = null is act(deterministic=True).
+struct ActArgs {
+  int B, S;
+  const float* states;  // [B][S]
+  const float* params;
+  int64_t off[13];
+  const float* noise;  // [B][2] standard normal, or null
+  float *action, *pre_tanh, *logp, *value;
+};
+
+template <int QH, int NW>
+__global__ void __launch_bounds__(64 * NW, 1) ppo_act(ActArgs r) {
+  constexpr int H = 64 * QH;
+  constexpr int RPW = kRowTile / NW;
+  constexpr int PH = H + 4, PA = 2 * H + 4, PXMAX = kMaxRowS + 4;
+  __shared__ __attribute__((aligned(16))) float X[kRowTile * PXMAX];
+  __shared__ __attribute__((aligned(16))) float H1[kRowTile * PH];
+  __shared__ __attribute__((aligned(16))) float H2[kRowTile * PH];
+  __shared__ __attribute__((aligned(16))) float AC[kRowTile * PA];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int row0 = blockIdx.x * kRowTile;
+  const int nrows = min(kRowTile, r.B - row0);
+  const float* P = r.params;
+  rows_forward<QH, NW>(r.states, nullptr, r.S, nrows, row0, P, r.off, X, H1, H2, AC, nullptr,
+                       nullptr, nullptr);
+  float wa0[QH], wa1[QH], wc[QH];
+#pragma unroll
+  for (int q = 0; q < QH; ++q) {
+    const int col = lane + 64 * q;
+    wa0[q] = P[r.off[P_WA2] + col];
+    wa1[q] = P[r.off[P_WA2] + H + col];
+    wc[q] = P[r.off[P_WC2] + col];
+  }
+  const float ba0 = P[r.off[P_BA2]], ba1 = P[r.off[P_BA2] + 1], bcv = P[r.off[P_BC2]];
+  const float ls0 = P[r.off[P_LOGSTD]], ls1 = P[r.off[P_LOGSTD] + 1];
+  const float sc0 = expf(ls0), sc1 = expf(ls1);
+  const float var0 = sc0 * sc0, var1 = sc1 * sc1;
+  const float lsc0 = logf(sc0), lsc1 = logf(sc1);
+  const float LOG_SQRT_2PI = 0.91893853320467274178f;
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int lr = RPW * w + rr;
+    if (lr >= nrows) break;
+    const int b = row0 + lr;
+    const float* arow = AC + lr * PA;
+    float p0 = 0.0f, p1 = 0.0f, pv = 0.0f;
+#pragma unroll
+    for (int q = 0; q < QH; ++q) {
+      const int col = lane + 64 * q;
+      const float a = arow[col], c = arow[H + col];
+      p0 += a * wa0[q];
+      p1 += a * wa1[q];
+      pv += c * wc[q];
+    }
+    const float mu0 = wave_sum(p0) + ba0, mu1 = wave_sum(p1) + ba1, val = wave_sum(pv) + bcv;
+    if (lane == 0) {
+      float z0 = mu0, z1 = mu1, lp = 0.0f;
+      if (r.noise) {
+        z0 = mu0 + sc0 * r.noise[2 * (long)b];
+        z1 = mu1 + sc1 * r.noise[2 * (long)b + 1];
+        const float d0 = z0 - mu0, d1 = z1 - mu1;
+        const float t0 = tanhf(z0), t1 = tanhf(z1);
+        const float lp0 = -(d0 * d0) / (2.0f * var0) - lsc0 - LOG_SQRT_2PI;
+        const float lp1 = -(d1 * d1) / (2.0f * var1) - lsc1 - LOG_SQRT_2PI;
+        lp = (lp0 - log1pf(-(t0 * t0) + 1e-6f)) + (lp1 - log1pf(-(t1 * t1) + 1e-6f));
+      }
+      r.action[2 * (long)b] = tanhf(z0);
+      r.action[2 * (long)b + 1] = tanhf(z1);
+      r.pre_tanh[2 * (long)b] = z0;
+      r.pre_tanh[2 * (long)b + 1] = z1;
+      r.logp[b] = lp;
+      r.value[b] = val;
+    }
+  }
 }
 
 // ----------------------------------------------------------------------------- weight grads
@@ -1505,6 +1603,31 @@ int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream) {
   o.lr = a->lr, o.beta1 = a->beta1, o.beta2 = a->beta2, o.eps = a->adam_eps;
   o.max_norm = a->max_grad_norm;
   hipLaunchKernelGGL(ppo_adam, dim3(w.nred), dim3(256), 0, s, o);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int hwy_ppo_act(const hwy_ppo_act_args* a, void* stream) {
+  if (!a || !a->states || !a->params || !a->action || !a->pre_tanh || !a->logp || !a->value)
+    return -1;
+  const hwy_ppo_dims& d = a->dims;
+  if (!fused_ok(d) || d.A != 2 || d.B < 1) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  const Layout L = make_layout(d);
+  ActArgs r = {};
+  r.B = d.B, r.S = d.S, r.states = a->states, r.params = a->params, r.noise = a->noise;
+  for (int i = 0; i < 13; ++i) r.off[i] = L.off[i];
+  r.action = a->action, r.pre_tanh = a->pre_tanh, r.logp = a->logp, r.value = a->value;
+  const dim3 g((d.B + kRowTile - 1) / kRowTile), b4(256), b8(512);
+  switch (d.H / 64) {
+    case 1: hipLaunchKernelGGL((ppo_act<1, 4>), g, b4, 0, s, r); break;
+    case 2: hipLaunchKernelGGL((ppo_act<2, 8>), g, b8, 0, s, r); break;
+    case 3: hipLaunchKernelGGL((ppo_act<3, 4>), g, b4, 0, s, r); break;
+    case 4: hipLaunchKernelGGL((ppo_act<4, 8>), g, b8, 0, s, r); break;
+    case 5: hipLaunchKernelGGL((ppo_act<5, 4>), g, b4, 0, s, r); break;
+    case 6: hipLaunchKernelGGL((ppo_act<6, 8>), g, b8, 0, s, r); break;
+    case 7: hipLaunchKernelGGL((ppo_act<7, 4>), g, b4, 0, s, r); break;
+    default: hipLaunchKernelGGL((ppo_act<8, 8>), g, b8, 0, s, r); break;
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

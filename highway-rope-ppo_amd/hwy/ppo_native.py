@@ -45,6 +45,15 @@ class PpoArgs(ctypes.Structure):
     ]
 
 
+class PpoActArgs(ctypes.Structure):
+    _fields_ = [
+        ("dims", PpoDims),
+        ("states", ctypes.c_void_p), ("params", ctypes.c_void_p), ("noise", ctypes.c_void_p),
+        ("action", ctypes.c_void_p), ("pre_tanh", ctypes.c_void_p), ("logp", ctypes.c_void_p),
+        ("value", ctypes.c_void_p),
+    ]
+
+
 def _bind(L):
     if getattr(L, "_ppo_bound", False):
         return L
@@ -56,6 +65,8 @@ def _bind(L):
     L.hwy_ppo_forward_backward.restype = ctypes.c_int
     L.hwy_ppo_optimizer.argtypes = [ctypes.POINTER(PpoArgs), ctypes.c_void_p]
     L.hwy_ppo_optimizer.restype = ctypes.c_int
+    L.hwy_ppo_act.argtypes = [ctypes.POINTER(PpoActArgs), ctypes.c_void_p]
+    L.hwy_ppo_act.restype = ctypes.c_int
     L._ppo_bound = True
     return L
 
@@ -71,6 +82,70 @@ def param_layout(S: int, H: int, B: int = 64):
     return list(offs), int(n.value)
 
 
+def flat_params(agent):
+    """The ActorCritic's parameters (and gradients) as views of one flat fp32 buffer in
+    hwy_ppo_param_layout order, created once per agent and shared by FusedPPO and fused_act."""
+    cached = getattr(agent, "_flat", None)
+    ac = agent.actor_critic
+    named = dict(ac.named_parameters())
+    if cached is not None and all(named[n].data.data_ptr() == cached[0][o:].data_ptr()
+                                  for n, o in zip(_PARAM_ORDER, cached[2])):
+        return cached
+    if set(named.keys()) != set(_PARAM_ORDER):
+        raise ValueError("unexpected ActorCritic parameter layout for the fused step")
+    S = named["shared.0.weight"].shape[1]
+    H = named["shared.0.weight"].shape[0]
+    if named["log_std"].numel() != 2:
+        raise ValueError("fused PPO step needs action_dim == 2")
+    offs, numel = param_layout(S, H)
+    dev = named["log_std"].device
+    flat = torch.empty(numel, device=dev, dtype=torch.float32)
+    grads = torch.zeros(numel, device=dev, dtype=torch.float32)
+    params: List[torch.nn.Parameter] = []
+    with torch.no_grad():
+        for name, off in zip(_PARAM_ORDER, offs):
+            p = named[name]
+            n = p.numel()
+            flat[off:off + n].copy_(p.detach().reshape(-1))
+            p.data = flat[off:off + n].view_as(p)
+            p.grad = grads[off:off + n].view_as(p)
+            params.append(p)
+    agent._flat = (flat, grads, offs, params)
+    agent._learner = None  # a torch-graph learner captured the old storage
+    return agent._flat
+
+
+def act_supported(S: int, H: int, A: int) -> bool:
+    return A == 2 and S % 4 == 0 and S <= 256 and H % 64 == 0 and 64 <= H <= 512
+
+
+def fused_act(agent, states: torch.Tensor, deterministic: bool = False,
+              generator: Optional[torch.Generator] = None):
+    """ActorCritic.act (ppo/agent.py:86-95) through hwy_ppo_act: one launch for the forward,
+    the Normal sample (noise drawn from `generator` exactly as act() draws it), tanh and the
+    squashed log-prob.  Returns (action, pre_tanh, log_prob, value)."""
+    flat = flat_params(agent)[0]
+    B, S = states.shape
+    H = agent.actor_critic.shared[0].weight.shape[0]
+    dev = states.device
+    states = states.contiguous()
+    noise = None
+    if not deterministic:
+        noise = torch.randn((B, 2), device=dev, dtype=states.dtype, generator=generator)
+    action = torch.empty(B, 2, device=dev)
+    pre = torch.empty(B, 2, device=dev)
+    logp = torch.empty(B, device=dev)
+    value = torch.empty(B, device=dev)
+    a = PpoActArgs()
+    a.dims = PpoDims(B, S, H, 2)
+    a.states, a.params = states.data_ptr(), flat.data_ptr()
+    a.noise = None if noise is None else noise.data_ptr()
+    a.action, a.pre_tanh, a.logp, a.value = (action.data_ptr(), pre.data_ptr(), logp.data_ptr(),
+                                             value.data_ptr())
+    check(_bind(lib()).hwy_ppo_act(ctypes.byref(a), stream_ptr()), "hwy_ppo_act")
+    return action, pre, logp, value
+
+
 class FusedPPO:
     def __init__(self, agent, mb: int, nmb: int, group=None, use_graphs: bool = True):
         ac = agent.actor_critic
@@ -84,28 +159,17 @@ class FusedPPO:
         if named["log_std"].numel() != 2:
             raise ValueError("fused PPO step needs action_dim == 2")
         self.S, self.H, self.mb, self.nmb = S, H, mb, nmb
-        offs, numel = param_layout(S, H, mb)
         L = _bind(lib())
         self.L = L
         self.dims = PpoDims(mb, S, H, 2)
         ws = L.hwy_ppo_workspace_bytes(ctypes.byref(self.dims))
         if ws < 0:
             raise ValueError("unsupported fused PPO dims")
-        self.flat = torch.empty(numel, device=dev, dtype=torch.float32)
-        self.grads = torch.zeros(numel, device=dev, dtype=torch.float32)
+        self.flat, self.grads, self.offs, self.params = flat_params(agent)
+        numel = self.flat.numel()
         self.m = torch.zeros(numel, device=dev, dtype=torch.float32)
         self.v = torch.zeros(numel, device=dev, dtype=torch.float32)
-        self.params: List[torch.nn.Parameter] = []
-        with torch.no_grad():
-            for name, off in zip(_PARAM_ORDER, offs):
-                p = named[name]
-                n = p.numel()
-                self.flat[off:off + n].copy_(p.detach().reshape(-1))
-                p.data = self.flat[off:off + n].view_as(p)
-                p.grad = self.grads[off:off + n].view_as(p)
-                self.params.append(p)
-        self.offs = offs
-        self.workspace = torch.zeros(int(ws), device=dev, dtype=torch.uint8)  # counters start at 0
+        self.workspace = torch.zeros(int(ws), device=dev, dtype=torch.uint8)
         self.counters = torch.zeros(2, device=dev, dtype=torch.int32)
         self.metrics = torch.zeros(max(1, agent.epochs * nmb), 6, device=dev)
         self.group = group

@@ -341,8 +341,25 @@ class PPOAgent:
     # ------------------------------------------------------------------ acting
     def select_action(self, state, deterministic: bool = False):
         if isinstance(state, torch.Tensor) and state.dim() == 2:
+            if self._act_fused_ok(state):
+                from hwy.ppo_native import fused_act
+
+                return fused_act(self, state, deterministic, self.generator)
             return self.actor_critic.act(state, deterministic, generator=self.generator)
         return self.actor_critic.get_action(state, deterministic)
+
+    def _act_fused_ok(self, state: torch.Tensor) -> bool:
+        """Batched acting runs through hwy_ppo_act (one launch) unless backend='torch'."""
+        if self.backend == "torch" or not state.is_cuda:
+            return False
+        from hwy.ppo_native import act_supported
+
+        H = self.actor_critic.shared[0].weight.shape[0]
+        ok = act_supported(state.shape[1], H, self.actor_critic.log_std.numel())
+        if not ok and self.backend == "hip":
+            raise ValueError("backend='hip' acting needs action_dim 2, state_dim % 4 == 0 "
+                             "(<= 256) and hidden_dim in {64,128,...,512}")
+        return ok
 
     # ------------------------------------------------------------------ metrics
     def _finish_metrics(self, rows: np.ndarray, sizes: List[int], values, returns) -> Dict[str, float]:

@@ -66,6 +66,23 @@ int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream);
 /* clip_grad_norm_(max_grad_norm) + Adam step on params (call after any gradient all-reduce). */
 int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream);
 
+/* ActorCritic.act on a batch (replaces ppo/agent.py:86-95's forward + Normal sample + tanh +
+ * squashed log-prob on the batched rollout path): dims.B rows of states [B][S] (contiguous);
+ * noise [B][2] standard-normal draws (the caller's generator, as act() draws them) or NULL for
+ * act(deterministic=True) (z = mean, log_prob = 0).  Needs S % 4 == 0, S <= 256,
+ * H in {64, 128, ..., 512}. */
+typedef struct hwy_ppo_act_args {
+  hwy_ppo_dims dims;
+  const float* states;
+  const float* params; /* flat, hwy_ppo_param_layout order */
+  const float* noise;
+  float* action;   /* [B][2] tanh(z) */
+  float* pre_tanh; /* [B][2] z */
+  float* logp;     /* [B] */
+  float* value;    /* [B] */
+} hwy_ppo_act_args;
+int hwy_ppo_act(const hwy_ppo_act_args* a, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
