@@ -43,7 +43,11 @@ __device__ unsigned long long g_ppo_sections[16];
       for (int _i = 0; _i < 16; ++_i)                                          \
         if (_pacc[_i]) atomicAdd(&g_ppo_sections[_i], _pacc[_i]);              \
   } while (0)
+#define PSEC_PARAMS , uint64_t &_pt, uint64_t *_pacc
+#define PSEC_ARGS , _pt, _pacc
 #else
+#define PSEC_PARAMS
+#define PSEC_ARGS
 #define PSEC_DECL
 #define PSEC(id) \
   do {           \
@@ -605,47 +609,112 @@ struct RowArgs {
 
 __device__ __forceinline__ int row_pitch(int n) { return n + 4; }  // n/4 + 1 odd: conflict-free
 
-template <int QH, bool NN>
-__device__ __forceinline__ void row_gemm(const float* act, int pa, int Kp, int K, const float* W,
-                                         int ldw, int n_base, f32x4 (&acc)[QH]) {
-  constexpr int D = QH <= 4 ? 4 : 2;  // 16-deep k blocks of weights in flight
-  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-#pragma unroll
-  for (int t = 0; t < QH; ++t) acc[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  f32x4 wbuf[D][QH];
-  auto load = [&](int kb, f32x4(&dst)[QH]) {
+// The weights of every layer a ppo_rows / ppo_act wave touches, as one stream of 16-deep k
+// blocks (segments = layers, in execution order).  D blocks stay in flight in registers and the
+// stream runs on across layer boundaries, barriers and the loss head, so a layer's first
+// weights are already loaded when its activations are ready.  Segment lengths are multiples of
+// D blocks (K is zero-padded: weights past K load as 0 and the activation images are zero-padded
+// to the padded K).
+#define H_TW(QH, NW) ((64 * (QH)) / (NW) / 16)
+
+struct WSeg {
+  const float* W;
+  int ldw, K, nblk, nn;  // nn: W is [K][N] (k-major), else [N][K]
+};
+
+template <int TW, int D, int NSEG>
+struct WRing {
+  f32x4 buf[D][TW];
+  WSeg sg[NSEG];
+  int n_base, g, c;
+
+  // Branch-free loads (so the compiler can count them): element (k, n) of segment s sits at
+  // W + n*sn + k*sk with (sn, sk) = (ldw, 1) for [N][K] and (1, ldw) for [K][N]; k past K is
+  // clamped into range here and zeroed when the block is consumed.
+  __device__ __forceinline__ void load_blk(const float* W, int ldw, int nn, int kb,
+                                           f32x4 (&dst)[TW]) {
     const int k = kb + 4 * g;
+    const long sn = nn ? 1 : ldw, sk = nn ? ldw : 1;
 #pragma unroll
-    for (int t = 0; t < QH; ++t) {
-      const int n = n_base + 16 * t + c;
-      if (k >= K) {
-        dst[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-      } else if (!NN) {
-        dst[t] = *reinterpret_cast<const f32x4*>(W + (long)n * ldw + k);
-      } else {
-        const float* p = W + (long)k * ldw + n;
-        dst[t] = f32x4{p[0], p[ldw], p[2 * ldw], p[3 * ldw]};
-      }
+    for (int t = 0; t < TW; ++t) {
+      const float* p = W + (long)(n_base + 16 * t + c) * sn + (long)k * sk;
+      dst[t] = f32x4{p[0], p[sk], p[2 * sk], p[3 * sk]};
     }
-  };
+  }
+  // load local block b of segment SEG, or (past its end) of the next segment; past the last
+  // segment a harmless in-range block (never consumed)
+  template <int SEG>
+  __device__ __forceinline__ void load_ahead(int b, f32x4 (&dst)[TW]) {
+    constexpr int NX = SEG + 1 < NSEG ? SEG + 1 : SEG;
+    const bool nxt = b >= sg[SEG].nblk;
+    const WSeg& s0 = sg[SEG];
+    const WSeg& s1 = sg[NX];
+    const float* W = nxt ? s1.W : s0.W;
+    const int ldw = nxt ? s1.ldw : s0.ldw, nn = nxt ? s1.nn : s0.nn, K = nxt ? s1.K : s0.K;
+    int kb = nxt ? 16 * (b - s0.nblk) : 16 * b;
+    if (SEG + 1 >= NSEG && nxt) kb = 0;
+    kb = min(kb, K - 4 - 4 * g);  // k + 3 < K for every lane (K % 4 == 0)
+    load_blk(W, ldw, nn, kb, dst);
+  }
+  __device__ __forceinline__ void prime() {
 #pragma unroll
-  for (int d = 0; d < D; ++d)
-    if (16 * d < Kp) load(16 * d, wbuf[d]);
-  for (int kb0 = 0; kb0 < Kp; kb0 += 16 * D) {
+    for (int d = 0; d < D; ++d) load_ahead<0>(d, buf[d]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // acc += act[16][16*nblk] (LDS, pitch pa) x segment SEG's weights for this wave's columns
+  template <int SEG>
+  __device__ __forceinline__ void run(const float* act, int pa, f32x4 (&acc)[TW]) {
+    const int nblk = sg[SEG].nblk;
+    const float* arow = act + c * pa + 4 * g;
+    f32x4 a_nxt = *reinterpret_cast<const f32x4*>(arow);
+    for (int b0 = 0; b0 < nblk; b0 += D) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const int kb = kb0 + 16 * d;
-      if (kb < Kp) {
-        const f32x4 a = *reinterpret_cast<const f32x4*>(act + c * pa + kb + 4 * g);
+      for (int d = 0; d < D; ++d) {
+        const int kb = 16 * (b0 + d);
+        const f32x4 a = a_nxt;  // activations of this block, read one block ahead
+        a_nxt = *reinterpret_cast<const f32x4*>(arow + min(kb + 16, 16 * (nblk - 1)));
+        const bool kin = kb + 4 * g < sg[SEG].K;  // else the block was clamped: weights are 0
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int t = 0; t < QH; ++t)
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], wbuf[d][t][j], acc[t], 0, 0, 0);
-        if (kb + 16 * D < Kp) load(kb + 16 * D, wbuf[d]);
+          for (int t = 0; t < TW; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], kin ? buf[d][t][j] : 0.0f,
+                                                          acc[t], 0, 0, 0);
+        // issue the refill here: the scheduler would otherwise sink it next to its use
+        __builtin_amdgcn_sched_barrier(0);
+        load_ahead<SEG>(b0 + d + D, buf[d]);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
+};
+
+template <int TW>
+__device__ __forceinline__ void zero_acc(f32x4 (&acc)[TW]) {
+#pragma unroll
+  for (int t = 0; t < TW; ++t) acc[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+}
+
+template <int TW>
+constexpr int ring_depth() { return TW <= 2 ? 4 : (TW <= 4 ? 4 : 2); }
+
+// segment table of the row kernels: forward W1, W2, Wa1, Wc1 ([N][K]); backward Wa1, Wc1, W2
+// read k-major for dh2 = dac [Wa1; Wc1] and dh1 = dh2 W2
+template <int TW, int D, int NSEG>
+__device__ __forceinline__ void ring_setup(WRing<TW, D, NSEG>& R, const float* P, const int64_t* off,
+                                           int S, int H, int n_base) {
+  const int lane = threadIdx.x & 63;
+  R.g = lane >> 4;
+  R.c = lane & 15;
+  R.n_base = n_base;
+  const int hb = (H / 16 + D - 1) / D * D;
+  const int sb = ((S + 15) / 16 + D - 1) / D * D;
+  const WSeg all[7] = {{P + off[P_W1], S, S, sb, 0},   {P + off[P_W2], H, H, hb, 0},
+                       {P + off[P_WA1], H, H, hb, 0},  {P + off[P_WC1], H, H, hb, 0},
+                       {P + off[P_WA1], H, H, hb, 1},  {P + off[P_WC1], H, H, hb, 1},
+                       {P + off[P_W2], H, H, hb, 1}};
+#pragma unroll
+  for (int i = 0; i < NSEG; ++i) R.sg[i] = all[i];
 }
 
 // C element (t, r) of lane: row 4*(lane>>4) + r, column n_base + 16 t + (lane & 15)
@@ -690,17 +759,19 @@ __device__ __forceinline__ void row_epi_mask(const f32x4 (&acc)[QH], float* mask
 // Forward of the 16 rows starting at row0 (rows idx[row0 + i], or row0 + i without idx) into
 // the LDS images X, H1, H2, AC = [a1 | c1]; optionally also to HBM (xg, h1, h2; null = no).
 // Ends with a workgroup barrier.
-template <int QH, int NW>
-__device__ __forceinline__ void rows_forward(const float* states, const int64_t* idx, int S,
-                                             int nrows, int row0, const float* P,
-                                             const int64_t* off, float* X, float* H1, float* H2,
-                                             float* AC, float* xg, float* h1g, float* h2g) {
+template <int QH, int NW, int D, int NSEG>
+__device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG>& R, const float* states,
+                                             const int64_t* idx, int S, int nrows, int row0,
+                                             const float* P, const int64_t* off, float* X,
+                                             float* H1, float* H2, float* AC, float* xg,
+                                             float* h1g, float* h2g PSEC_PARAMS) {
   constexpr int H = 64 * QH;
-  constexpr int TW = H / NW / 16;
+  constexpr int TW = H_TW(QH, NW);
   constexpr int NT = 64 * NW;
   constexpr int PH = H + 4, PA = 2 * H + 4;
-  const int t = threadIdx.x, w = t >> 6;
-  const int Sp = (S + 15) / 16 * 16, px = row_pitch(Sp);
+  const int t = threadIdx.x;
+  // zero-padded to whole ring groups of 16-deep blocks
+  const int Sp = ((S + 15) / 16 + D - 1) / D * D * 16, px = row_pitch(Sp);
   // states rows, zero-padded to Sp columns and 16 rows
   for (int e = t; e < kRowTile * (Sp / 4); e += NT) {
     const int row = e / (Sp / 4), k = 4 * (e % (Sp / 4));
@@ -713,22 +784,29 @@ __device__ __forceinline__ void rows_forward(const float* states, const int64_t*
     *reinterpret_cast<f32x4*>(&X[row * px + k]) = v;
   }
   __syncthreads();
-  const int nb = w * (H / NW);  // this wave's output columns of an H-wide layer
+  PSEC(0);
+  const int nb = R.n_base;  // this wave's output columns of an H-wide layer
   f32x4 acc[TW];
   // h1 = relu(x W1^T + b1)
-  row_gemm<TW, false>(X, px, Sp, S, P + off[P_W1], S, nb, acc);
+  zero_acc(acc);
+  R.template run<0>(X, px, acc);
   row_epi_bias_relu<TW>(acc, P + off[P_B1], H1, PH, h1g ? h1g + (long)row0 * H : nullptr, H,
                         nrows, nb);
   __syncthreads();
+  PSEC(1);
   // h2 = relu(h1 W2^T + b2)
-  row_gemm<TW, false>(H1, PH, H, H, P + off[P_W2], H, nb, acc);
+  zero_acc(acc);
+  R.template run<1>(H1, PH, acc);
   row_epi_bias_relu<TW>(acc, P + off[P_B2], H2, PH, h2g ? h2g + (long)row0 * H : nullptr, H,
                         nrows, nb);
   __syncthreads();
+  PSEC(2);
   // [a1 | c1] = relu(h2 [Wa1; Wc1]^T + [ba1; bc1])
-  row_gemm<TW, false>(H2, PH, H, H, P + off[P_WA1], H, nb, acc);
+  zero_acc(acc);
+  R.template run<2>(H2, PH, acc);
   row_epi_bias_relu<TW>(acc, P + off[P_BA1], AC, PA, nullptr, 0, nrows, nb);
-  row_gemm<TW, false>(H2, PH, H, H, P + off[P_WC1], H, nb, acc);
+  zero_acc(acc);
+  R.template run<3>(H2, PH, acc);
   row_epi_bias_relu<TW>(acc, P + off[P_BC1], AC + H, PA, nullptr, 0, nrows, nb);
   __syncthreads();
 }
@@ -753,8 +831,12 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   const int row0 = blockIdx.x * kRowTile;
   const int nrows = min(kRowTile, r.B - row0);
   const float* P = r.params;
-  rows_forward<QH, NW>(r.states, r.idx, S, nrows, row0, P, r.off, X, H1, H2, AC, r.xg, r.h1,
-                       r.h2);
+  constexpr int D = ring_depth<TW>();
+  WRing<TW, D, 7> R;
+  ring_setup(R, P, r.off, S, H, w * (H / NW));
+  R.prime();
+  rows_forward<QH, NW>(R, r.states, r.idx, S, nrows, row0, P, r.off, X, H1, H2, AC, r.xg, r.h1,
+                       r.h2 PSEC_ARGS);
   PSEC(3);
   const int nb = w * (H / NW);  // this wave's output columns of an H-wide layer
   f32x4 acc[TW];
@@ -853,13 +935,9 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   PSEC(4);
   // dh2 = (dac [Wa1; Wc1]) * (h2 > 0)   ([Wa1; Wc1] is [2H][H]: k-major); the two halves of
   // K = 2H (Wa1 rows, Wc1 rows) are summed at the end
-  {
-    f32x4 acc2[TW];
-    row_gemm<TW, true>(AC, PA, H, H, P + r.off[P_WA1], H, nb, acc);
-    row_gemm<TW, true>(AC + H, PA, H, H, P + r.off[P_WC1], H, nb, acc2);
-#pragma unroll
-    for (int q = 0; q < TW; ++q) acc[q] = acc[q] + acc2[q];
-  }
+  zero_acc(acc);
+  R.template run<4>(AC, PA, acc);
+  R.template run<5>(AC + H, PA, acc);
   row_epi_mask<TW>(acc, H2, PH, true, r.dh2 + (long)row0 * H, H, nrows, nb);
   __syncthreads();
   PSEC(5);
@@ -888,7 +966,8 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
     }
   }
   // dh1 = (dh2 W2) * (h1 > 0)
-  row_gemm<TW, true>(H2, PH, H, H, P + r.off[P_W2], H, nb, acc);
+  zero_acc(acc);
+  R.template run<6>(H2, PH, acc);
   row_epi_mask<TW>(acc, H1, PH, false, r.dh1 + (long)row0 * H, H, nrows, nb);
   PSEC(6);
   PSEC_FLUSH;
@@ -920,8 +999,16 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_act(ActArgs r) {
   const int row0 = blockIdx.x * kRowTile;
   const int nrows = min(kRowTile, r.B - row0);
   const float* P = r.params;
-  rows_forward<QH, NW>(r.states, nullptr, r.S, nrows, row0, P, r.off, X, H1, H2, AC, nullptr,
-                       nullptr, nullptr);
+  constexpr int TW = H_TW(QH, NW);
+  constexpr int D = ring_depth<TW>();
+  WRing<TW, D, 4> R;
+  ring_setup(R, P, r.off, r.S, H, w * (H / NW));
+  R.prime();
+#ifdef HWY_SECTION_PROFILE
+  uint64_t _pt = 0, _pacc[16];
+#endif
+  rows_forward<QH, NW>(R, r.states, nullptr, r.S, nrows, row0, P, r.off, X, H1, H2, AC, nullptr,
+                       nullptr, nullptr PSEC_ARGS);
   float wa0[QH], wa1[QH], wc[QH];
 #pragma unroll
   for (int q = 0; q < QH; ++q) {
