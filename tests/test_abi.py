@@ -1,5 +1,5 @@
-"""C ABI boundary: libhwy.so loads (no GPU needed), exports every function include/hwy.h
-declares, and agrees with the Python/ctypes mirror on the config layout."""
+"""C ABI boundary: libhwy.so loads (no GPU needed), exports every function include/*.h
+declares, and agrees with the Python/ctypes mirror on the config and PPO parameter layouts."""
 
 import ctypes
 import os
@@ -11,14 +11,18 @@ from hwy import _abi
 from hwy.native import LIB_PATH
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "hwy.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in sorted(os.listdir(os.path.join(ROOT, "include")))
+           if h.endswith(".h")]
 
 
 def declared_functions():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\**\s+(hwy_[a-z_0-9]+)\s*\(", src, flags=re.M)
-    return sorted(set(names))
+    names = set()
+    for header in HEADERS:
+        src = open(header).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names.update(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\**\s+(hwy_[a-z_0-9]+)\s*\(", src,
+                                flags=re.M))
+    return sorted(names)
 
 
 @pytest.fixture(scope="module")
@@ -32,7 +36,10 @@ def test_header_declares_the_boundary():
     for must in ["hwy_create", "hwy_destroy", "hwy_reset", "hwy_step", "hwy_obs_pe", "hwy_gae",
                  "hwy_set_pe_table", "hwy_export_state", "hwy_import_state", "hwy_last_error"]:
         assert must in names
-    assert len(names) >= 15
+    for must in ["hwy_ppo_param_layout", "hwy_ppo_workspace_bytes", "hwy_ppo_forward_backward",
+                 "hwy_ppo_optimizer", "hwy_ppo_act"]:
+        assert must in names
+    assert len(names) >= 20
 
 
 def test_every_declared_symbol_is_exported(lib):
@@ -72,3 +79,21 @@ def test_no_cpu_fallback_in_product_path():
             if f.endswith(".py"):
                 text = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", text, flags=re.M), f
+
+
+def test_ppo_param_layout_matches_actor_critic():
+    """hwy_ppo_param_layout (host-only) equals nn.Module.parameters() sizes in _PARAM_ORDER."""
+    import torch
+
+    from hwy.ppo_native import _PARAM_ORDER, param_layout
+    from ppo.agent import ActorCritic
+
+    for S, H in [(60, 256), (120, 64), (136, 512)]:
+        ac = ActorCritic(S, 2, H)
+        named = dict(ac.named_parameters())
+        offs, numel = param_layout(S, H)
+        sizes = [named[n].numel() for n in _PARAM_ORDER]
+        assert offs == [sum(sizes[:i]) for i in range(13)]
+        assert numel == sum(sizes) == sum(p.numel() for p in ac.parameters())
+    with pytest.raises(ValueError):
+        param_layout(60, 100)  # hidden_dim not a multiple of 64
