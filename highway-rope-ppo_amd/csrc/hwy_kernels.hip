@@ -564,6 +564,28 @@ __device__ void road_order(int lane, const Veh& v, uint64_t pres, RoadOrder& o) 
     kp = shf64(key, o.ord);
     kn = shf64(kp, nxt);
     sorted = !wave_any(lane < WAVE - 1 && !(kp < kn));
+    // a few overtakes since the last frame: odd-even transposition rounds on (key, vehicle)
+    // in position space usually restore the order without a full re-rank
+    int ordp = o.ord;
+    for (int round = 0; round < 3 && !sorted; ++round) {
+#pragma unroll
+      for (int ph = 0; ph < 2; ++ph) {
+        const bool left = (lane & 1) == ph;
+        int partner = left ? lane + 1 : lane - 1;
+        if (partner < 0 || partner >= WAVE) partner = lane;
+        const uint64_t pk = shf64(kp, partner);
+        const int po = shi(ordp, partner);
+        const bool swap = partner != lane && (left ? (pk < kp) : (kp < pk));
+        kp = swap ? pk : kp;
+        ordp = swap ? po : ordp;
+      }
+      kn = shf64(kp, nxt);
+      sorted = !wave_any(lane < WAVE - 1 && !(kp < kn));
+    }
+    if (sorted) {
+      o.ord = ordp;
+      o.rk = __builtin_amdgcn_ds_permute(ordp << 2, lane);  // vehicle ordp sits at position lane
+    }
   }
   if (!sorted) {
     int r = 0;

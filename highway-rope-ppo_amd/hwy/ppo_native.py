@@ -174,6 +174,7 @@ class FusedPPO:
         self.metrics = torch.zeros(max(1, agent.epochs * nmb), 6, device=dev)
         self.group = group
         self.world = 1 if group is None else torch.distributed.get_world_size(group)
+        self._avg_op = group is not None and torch.distributed.get_backend(group) == "nccl"
         self.use_graphs = use_graphs
         self._import_torch_state()
         self._graphs = None
@@ -232,8 +233,12 @@ class FusedPPO:
         check(self.L.hwy_ppo_optimizer(ctypes.byref(a), stream_ptr()), "hwy_ppo_optimizer")
 
     def _allreduce(self):
-        torch.distributed.all_reduce(self.grads, group=self.group)
-        self.grads.div_(self.world)
+        if self._avg_op:  # RCCL averages in the collective (no extra division kernel)
+            torch.distributed.all_reduce(self.grads, op=torch.distributed.ReduceOp.AVG,
+                                         group=self.group)
+        else:
+            torch.distributed.all_reduce(self.grads, group=self.group)
+            self.grads.div_(self.world)
 
     def run(self, states, pre_tanh, old_lp, adv, ret, perm: torch.Tensor) -> torch.Tensor:
         """All epochs of one update; returns the [epochs*nmb, 6] metrics rows (device)."""

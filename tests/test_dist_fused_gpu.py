@@ -1,0 +1,92 @@
+"""The fused HIP update's data-parallel path (FusedPPO with a process group: graph(forward +
+backward) -> all-reduce of the flat gradient -> graph(clip + Adam)) with 2 ranks on one GPU
+(gloo carries the all-reduce; on a node the same code runs over RCCL).  The sharded update must
+keep the replicas identical and equal one process on the concatenated minibatches."""
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+S, H, EPOCHS, NMB, NLOC = 60, 128, 2, 4, 1024
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _data(rank, dev):
+    g = torch.Generator(device="cpu").manual_seed(100 + rank)
+    d = dict(s=torch.randn(NLOC, S, generator=g), z=torch.randn(NLOC, 2, generator=g) * 0.5,
+             lp=torch.randn(NLOC, generator=g) - 2.0, a=torch.randn(NLOC, generator=g),
+             r=torch.randn(NLOC, generator=g), perm=torch.randperm(NLOC, generator=g))
+    return {k: v.to(dev) for k, v in d.items()}
+
+
+def _agent(dev, group=None):
+    from ppo.agent import PPOAgent
+
+    torch.manual_seed(7)
+    return PPOAgent(S, 2, lr=3e-4, epochs=EPOCHS, hidden_dim=H, device=dev, num_minibatches=NMB,
+                    use_graphs=True, process_group=group, backend="hip")
+
+
+def _worker(rank, world, port, out_dir):
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.join(os.path.dirname(here), "highway-rope-ppo_amd"), here]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    if rank == 1:
+        torch.manual_seed(999)  # different local init: the broadcast must make weights equal
+    from hwy.ppo_native import FusedPPO
+
+    agent = _agent(dev, torch.distributed.group.WORLD)
+    d = _data(rank, dev)
+    adv = agent.normalize_advantages(d["a"])
+    F = FusedPPO(agent, NLOC // NMB, NMB, group=torch.distributed.group.WORLD, use_graphs=True)
+    F.run(d["s"], d["z"].contiguous(), d["lp"], adv.contiguous(), d["r"], d["perm"])
+    torch.cuda.synchronize()
+    torch.save({"state": {k: v.cpu() for k, v in agent.actor_critic.state_dict().items()},
+                "adv": adv.cpu()}, os.path.join(out_dir, f"rank{rank}.pt"))
+    torch.distributed.destroy_process_group()
+
+
+def test_fused_sharded_update_equals_single_process(tmp_path):
+    port = _free_port()
+    mp.start_processes(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    for k in r0["state"]:  # replicas stay identical
+        torch.testing.assert_close(r0["state"][k], r1["state"][k], rtol=0, atol=0)
+    from hwy.ppo_native import FusedPPO
+
+    dev = torch.device("cuda", 0)
+    d0, d1 = _data(0, dev), _data(1, dev)
+    cat = {k: torch.cat([d0[k], d1[k]]) for k in ("s", "z", "lp", "a", "r")}
+    adv = (cat["a"] - cat["a"].mean()) / (cat["a"].std() + 1e-8)
+    torch.testing.assert_close(torch.cat([r0["adv"], r1["adv"]]).to(dev), adv, rtol=1e-5, atol=1e-6)
+    mb = NLOC // NMB
+    perm = torch.cat([torch.cat([d0["perm"][i * mb:(i + 1) * mb], d1["perm"][i * mb:(i + 1) * mb] + NLOC])
+                      for i in range(NMB)])
+    agent = _agent(dev)
+    F = FusedPPO(agent, 2 * mb, NMB, use_graphs=True)
+    F.run(cat["s"], cat["z"].contiguous(), cat["lp"], adv.contiguous(), cat["r"], perm.contiguous())
+    torch.cuda.synchronize()
+    steps = EPOCHS * NMB
+    for k, v in agent.actor_critic.state_dict().items():
+        dd = (r0["state"][k].to(dev) - v).abs()
+        # Adam normalises each element's step, so fp32 noise in near-zero gradients can move an
+        # element by up to ~lr per step: bound the worst case, require nearly all to agree
+        assert dd.max().item() <= 2 * 3e-4 * steps, k
+        assert (dd > 2e-5).float().mean().item() < 0.05, (k, dd.max().item())
