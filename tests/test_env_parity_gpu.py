@@ -175,3 +175,44 @@ def test_imported_state_roundtrip_and_step():
             assert d is None, f"step {t}: {d}"
     finally:
         hip.close()
+
+
+@pytest.mark.parametrize("E,N,order,pe,d", [(4096, None, "sorted", _abi.PE_NONE, 0),
+                                            (16384, 30, "shuffled", _abi.PE_ROPE, 4)])
+def test_full_size_env_blocks_match_oracle(E, N, order, pe, d):
+    """BASELINE configs[1] / configs[2] at full size: the whole batch steps on the GPU with
+    autoreset, and three 16-env blocks (start, middle, end) are replayed on the oracle from the
+    GPU's reset state with the blocks' global env indices (env_offset) -- every word equal."""
+    cfg = make_cfg(E=E, order=order, pe=pe, d=d, N=N)
+    table = pe_table_for(pe, d, cfg.obs_vehicles) if pe != _abi.PE_NONE else None
+    hip = HipEnv(cfg, table)
+    steps = 6
+    try:
+        hip.reset()
+        st0 = hip.state()
+        rng = np.random.default_rng(11)
+        acts = [rng.uniform(-1, 1, (E, 2)).astype(np.float32) for _ in range(steps)]
+        outs = []
+        for a in acts:
+            o = hip.step(a)
+            outs.append(tuple(x.copy() for x in o))
+        st_end = hip.state()
+    finally:
+        hip.close()
+    V = cfg.vehicles_count + 1
+    B = 16
+    for off in (0, E // 2 - B // 2, E - B):
+        sub = make_cfg(E=B, order=order, pe=pe, d=d, N=N)
+        sub.env_offset = off
+        sub.seed_stride = cfg.seed_stride
+        ora = OracleEnv(sub, table)
+        ora.state[:] = st0[:, off:off + B, :]
+        for t, a in enumerate(acts):
+            ro = ora.step(a[off:off + B])
+            rh = outs[t]
+            np.testing.assert_array_equal(rh[0][off:off + B], ro[0], err_msg=f"obs, block {off} step {t}")
+            np.testing.assert_array_equal(rh[1][off:off + B], ro[1], err_msg=f"reward, block {off}")
+            np.testing.assert_array_equal(rh[2][off:off + B].astype(bool), ro[2])
+            np.testing.assert_array_equal(rh[3][off:off + B].astype(bool), ro[3])
+        d_ = diff_state(st_end[:, off:off + B, :], ora.state, V)
+        assert d_ is None, f"block {off}: {d_}"

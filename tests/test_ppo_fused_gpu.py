@@ -50,7 +50,7 @@ def _torch_grad(agent, s, z, lp, adv, ret, idx):
     return L.flat_grad.clone(), L.metrics[0].clone()
 
 
-@pytest.mark.parametrize("S,H,mb", [(60, 256, 512), (60, 64, 256), (120, 512, 256), (136, 128, 128),
+@pytest.mark.parametrize("S,H,mb", [(60, 256, 4096), (60, 64, 256), (120, 512, 256), (136, 128, 128),
                                     (60, 192, 200), (30, 128, 256)])  # last: split-K path (S % 4)
 def test_fused_gradient_matches_autograd(S, H, mb):
     a, b = _agents(S, H)
