@@ -535,7 +535,6 @@ __device__ __forceinline__ void store_env_words(uint32_t* st, size_t fstride, ui
 struct RoadOrder {
   int rk, ord;
   bool valid;
-  bool tie;  // two present vehicles share an x, or an x is NaN (see road_order)
 };
 
 __device__ __forceinline__ uint64_t shf64(uint64_t v, int src) {
@@ -552,17 +551,14 @@ __device__ __forceinline__ uint64_t road_key(float x, bool present, int lane) {
   return ((uint64_t)s << 32) | (uint32_t)(WAVE - 1 - lane);
 }
 
-// Re-validates (or rebuilds) the order for the current positions.  Sets o.tie when two
-// present vehicles share an x or an x is NaN: the callers then take the sequential scans, whose
-// tie-breaking the bit-mask neighbour search below does not reproduce.
+// Re-validates (or rebuilds) the order for the current positions.
 __device__ void road_order(int lane, const Veh& v, uint64_t pres, RoadOrder& o) {
   const uint64_t key = road_key(v.x, v.present, lane);
   const int nxt = lane < WAVE - 1 ? lane + 1 : lane;
-  uint64_t kp = 0ull, kn = 0ull;
   bool sorted = false;
   if (o.valid) {
-    kp = shf64(key, o.ord);
-    kn = shf64(kp, nxt);
+    uint64_t kp = shf64(key, o.ord);
+    uint64_t kn = shf64(kp, nxt);
     sorted = !wave_any(lane < WAVE - 1 && !(kp < kn));
     // a few overtakes since the last frame: odd-even transposition rounds on (key, vehicle)
     // in position space usually restore the order without a full re-rank
@@ -603,36 +599,57 @@ __device__ void road_order(int lane, const Veh& v, uint64_t pres, RoadOrder& o) 
     o.rk = r;
     o.ord = __builtin_amdgcn_ds_permute(r << 2, lane);
     o.valid = true;
-    kp = shf64(key, o.ord);
-    kn = shf64(kp, nxt);
   }
-  const int npres = __popcll(pres);
-  const bool tie = lane + 1 < npres && (uint32_t)(kp >> 32) == (uint32_t)(kn >> 32);
-  o.tie = wave_any(tie || (v.present && v.x != v.x));
 }
 
 // Road.neighbour_vehicles(self, lane c) for c = ln-1, ln, ln+1 (slot s <-> c = ln-1+s) from the
 // road order: for each lane c a 64-bit mask over positions of the vehicles with
-// on_lane(c, margin 1); the front vehicle is the next set position above this one, the rear
-// the previous set position below (exact while no two x are equal, see road_order).
+// on_lane(c, margin 1).  Upstream scans the list in index order with `s <= s_v and s_v <=
+// s_front` (front: nearest x ahead or level, the LAST such vehicle on a tie) and `s_v < s and
+// s_v > s_rear` (rear: nearest x strictly behind, the FIRST on a tie).  Equal x sit together in
+// the order by descending index, so with g = the first position of this vehicle's x group the
+// front is the lowest set position >= g other than its own, the rear the highest below g.  NaN
+// positions fail on_lane; a vehicle at NaN itself finds nothing (every comparison is false).
+struct LaneScan {
+  float yp;      // y of the vehicle at position `lane`
+  bool okp;      // that vehicle is present and inside the road's x range
+  uint64_t ahead, behind;  // candidate positions for the front / the rear of this vehicle
+};
+
+__device__ __forceinline__ LaneScan lane_scan(int lane, const Veh& v, uint64_t pres,
+                                              const RoadOrder& o) {
+  LaneScan L;
+  const int npres = __popcll(pres);
+  const float xp = shf(v.x, o.ord);
+  L.yp = shf(v.y, o.ord);
+  L.okp = lane < npres && -LANE_VEH_LEN <= xp && xp < ROAD_LENGTH + LANE_VEH_LEN;
+  const float xprev = shf(xp, lane > 0 ? lane - 1 : 0);
+  const uint64_t starts = ballot(lane == 0 || !(xprev == xp));  // x-group starts (bit 0 set)
+  const int g = 63 - __builtin_clzll(starts & ((2ull << o.rk) - 1ull));  // rk = 63: all ones
+  const bool selfok = v.x == v.x;
+  L.ahead = selfok ? (~0ull << g) & ~(1ull << o.rk) : 0ull;
+  L.behind = selfok ? (1ull << g) - 1ull : 0ull;
+  return L;
+}
+
+__device__ __forceinline__ uint64_t on_lane_mask(const LaneScan& L, int c) {
+  return ballot(L.okp && hm_absf(lane_lat(L.yp, c)) <= LANE_WIDTH / 2.0f + 1.0f);
+}
+
 __device__ __forceinline__ void neighbours_ordered(const hwy_config& C, int lane, const Veh& v,
                                                    uint64_t pres, const RoadOrder& o, int fi[3],
                                                    int ri[3]) {
-  const int npres = __popcll(pres);
-  const float xp = shf(v.x, o.ord), yp = shf(v.y, o.ord);
-  const bool okp = lane < npres && -LANE_VEH_LEN <= xp && xp < ROAD_LENGTH + LANE_VEH_LEN;
+  const LaneScan L = lane_scan(lane, v, pres, o);
   uint64_t m[3] = {0ull, 0ull, 0ull};
   for (int c = 0; c < C.lanes_count; ++c) {
-    const uint64_t mc = ballot(okp && hm_absf(lane_lat(yp, c)) <= LANE_WIDTH / 2.0f + 1.0f);
+    const uint64_t mc = on_lane_mask(L, c);
 #pragma unroll
     for (int s = 0; s < 3; ++s)
       if (c == v.ln - 1 + s) m[s] = mc;
   }
-  const uint64_t above = o.rk >= WAVE - 1 ? 0ull : (~0ull << (o.rk + 1));
-  const uint64_t below = (1ull << o.rk) - 1ull;
 #pragma unroll
   for (int s = 0; s < 3; ++s) {
-    const uint64_t fa = m[s] & above, rb = m[s] & below;
+    const uint64_t fa = m[s] & L.ahead, rb = m[s] & L.behind;
     const int qf = fa ? __builtin_ctzll(fa) : 0;
     const int qr = rb ? 63 - __builtin_clzll(rb) : 0;
     const int vf = shi(o.ord, qf), vr = shi(o.ord, qr);
@@ -641,30 +658,18 @@ __device__ __forceinline__ void neighbours_ordered(const hwy_config& C, int lane
   }
 }
 
-// the same query by the sequential definition (one pass over the vehicles in index order)
-__device__ __forceinline__ void neighbours_scan(const hwy_config& C, int lane, const Veh& v,
-                                             uint64_t pres, int fi[3], int ri[3]) {
-  const int V = C.vehicles_count + 1;
-  float fsv[3] = {0.0f, 0.0f, 0.0f}, rsv[3] = {0.0f, 0.0f, 0.0f};
-#pragma unroll
-  for (int s = 0; s < 3; ++s) fi[s] = ri[s] = -1;
-  for (int k = 0; k < V; ++k) {
-    if (!((pres >> k) & 1ull)) continue;
-    const float xk = rdlf(v.x, k), yk = rdlf(v.y, k);
-    const bool ok = (k != lane) && (-LANE_VEH_LEN <= xk) && (xk < ROAD_LENGTH + LANE_VEH_LEN);
-#pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      const bool on = ok && hm_absf(lane_lat(yk, v.ln - 1 + s)) <= LANE_WIDTH / 2.0f + 1.0f;
-      if (on && v.x <= xk && (fi[s] < 0 || xk <= fsv[s])) {
-        fsv[s] = xk;
-        fi[s] = k;
-      }
-      if (on && xk < v.x && (ri[s] < 0 || xk > rsv[s])) {
-        rsv[s] = xk;
-        ri[s] = k;
-      }
-    }
+// the front vehicle on an arbitrary lane c of each vehicle (same rule as neighbours_ordered)
+__device__ __forceinline__ int front_on_lane(const hwy_config& C, int lane, const Veh& v,
+                                             uint64_t pres, const RoadOrder& o, int c_own) {
+  const LaneScan L = lane_scan(lane, v, pres, o);
+  uint64_t m = 0ull;
+  for (int c = 0; c < C.lanes_count; ++c) {
+    const uint64_t mc = on_lane_mask(L, c);
+    if (c == c_own) m = mc;
   }
+  const uint64_t fa = m & L.ahead;
+  const int vf = shi(o.ord, fa ? __builtin_ctzll(fa) : 0);
+  return fa ? vf : -1;
 }
 
 // per-wave LDS of the collision pass (5.2 KB)
@@ -678,7 +683,6 @@ struct CollLds {
 // Road.act() then Road.step(dt) for the env of this wave (lane = vehicle).
 __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, RoadOrder& ro,
                            float& cos_h, float& sin_h, CollLds& cl, SecProf& sp) {
-  const int V = C.vehicles_count + 1;
   const int lanes = C.lanes_count;
   const float limit = C.speed_limit;
   const float ch = cos_h, sh = sin_h;  // cos / sin of v.h (carried from the previous frame)
@@ -696,10 +700,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, Road
   SEC(sp, 0);
   if (!ro.valid) road_order(lane, v, pres, ro);  // later frames: validated after the last move
   SEC(sp, 9);
-  if (ro.tie)
-    neighbours_scan(C, lane, v, pres, fi, ri);
-  else
-    neighbours_ordered(C, lane, v, pres, ro, fi, ri);
+  neighbours_ordered(C, lane, v, pres, ro, fi, ri);
   SEC(sp, 1);
 
   // gathers (all lanes active)
@@ -785,19 +786,8 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, Road
   if (v.tl == v.ln - 1) ft = fi[0];
   if (v.tl == v.ln + 1) ft = fi[2];
   const bool extra = need_t && !(v.tl == v.ln - 1 || v.tl == v.ln + 1);
-  if (wave_any(extra)) {  // target lane not adjacent (rare): dedicated scan
-    float fsx = 0.0f;
-    int fx = -1;
-    for (int k = 0; k < V; ++k) {
-      if (!((pres >> k) & 1ull)) continue;
-      const float xk = rdlf(v.x, k), yk = rdlf(v.y, k);
-      const bool on = (k != lane) && (-LANE_VEH_LEN <= xk) && (xk < ROAD_LENGTH + LANE_VEH_LEN) &&
-                      hm_absf(lane_lat(yk, v.tl)) <= LANE_WIDTH / 2.0f + 1.0f;
-      if (on && v.x <= xk && (fx < 0 || xk <= fsx)) {
-        fsx = xk;
-        fx = k;
-      }
-    }
+  if (wave_any(extra)) {  // target lane not adjacent (rare): its own lane mask
+    const int fx = front_on_lane(C, lane, v, pres, ro, v.tl);
     if (extra) ft = fx;
   }
   const int st_ = ft >= 0 ? ft : lane;
@@ -867,9 +857,11 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, Road
   const float xbound = wave_any(nonfinite) ? __builtin_huge_valf()
                                            : (VEH_DIAGONAL + vabs * dt) * 1.001f + 1.0e-3f;
   uint64_t pm = 0ull;
-  if (!ro.tie) {
+  {
     // x-sorted road order: the candidates of a vehicle are the run of positions around its
     // own whose |dx| stays within the bound; walk both ways until every lane has left its run
+    // (equal x sit together; a NaN x, or any non-finite value, makes the bound infinite so
+    // the walk covers every present vehicle)
     const int npres = __popcll(pres);
     const float xs = shf(v.x, ro.ord);  // x at position `lane`
     bool up = v.present, dn = v.present;
@@ -882,14 +874,6 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, Road
       dn = dn && ro.rk - o >= 0 && !(hm_absf(xd - v.x) > xbound);
       if (up) pm |= 1ull << iu;
       if (dn) pm |= 1ull << id;
-    }
-  } else {
-    // |dx| is symmetric in the pair, so the ballot over lanes for vehicle k is k's own row
-    for (int k = 0; k < V; ++k) {
-      if (!((pres >> k) & 1ull)) continue;
-      const float xk = rdlf(v.x, k);
-      const uint64_t row = ballot(v.present && k != lane && !(hm_absf(xk - v.x) > xbound));
-      if (lane == k) pm = row;
     }
   }
   SEC(sp, 10);
@@ -994,7 +978,6 @@ __global__ void __launch_bounds__(256, 4) hwy_step_kernel(StepParams P) {
   ro.rk = lane;
   ro.ord = lane;
   ro.valid = false;
-  ro.tie = false;
   float cos_h, sin_h;
   hm_sincosf(v.h, &sin_h, &cos_h);
   SEC(sp, 15);

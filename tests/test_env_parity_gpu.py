@@ -177,6 +177,60 @@ def test_imported_state_roundtrip_and_step():
         hip.close()
 
 
+def _same_words(a, b, V):
+    """diff_state with every NaN word equal to every other (payloads are not specified)."""
+    a = a.view(np.uint32).copy()
+    b = b.view(np.uint32).copy()
+    for x in (a, b):
+        f = x[:9].view(np.float32)
+        f[np.isnan(f)] = np.float32(np.nan)
+    return diff_state(a, b, V)
+
+
+def test_equal_positions_and_nan():
+    """Vehicles sharing an x (the reference's neighbour search breaks such ties by list order:
+    front = the last of the nearest-ahead, rear = the first of the nearest-behind), -0/+0,
+    groups of three, the ego in a tie, and a NaN position."""
+    E = 24
+    cfg = make_cfg(E=E)
+    ora = OracleEnv(cfg)
+    ora.reset()
+    rng = np.random.default_rng(11)
+    st = ora.state.copy()
+    V = cfg.vehicles_count + 1
+    x = st[_abi.F_X].view(np.float32)
+    y = st[_abi.F_Y].view(np.float32)
+    spd = st[_abi.F_SPEED].view(np.float32)
+    for e in range(16):
+        for _ in range(int(rng.integers(3, 8))):
+            i, j = rng.choice(V, size=2, replace=False)
+            x[e, j] = x[e, i]
+            if rng.random() < 0.2:  # same spot and speed: a pile-up starting inside each other
+                y[e, j] = y[e, i]
+                spd[e, j] = spd[e, i]
+    for e in range(16, 20):
+        i, j, k = rng.choice(np.arange(1, V), size=3, replace=False)
+        x[e, j] = x[e, k] = x[e, i]
+    x[20, 3], x[20, 7], x[20, 9] = 0.0, -0.0, 0.0
+    x[21, 5] = x[21, 0]
+    x[21, 12] = x[21, 0]
+    x[22, 4] = np.nan
+    x[23, 17] = np.nan
+    x[23, 18] = x[23, 19]
+    ora.state[...] = st
+    hip = HipEnv(cfg)
+    try:
+        hip.set_state(st)
+        for t in range(12):
+            a = policy_actions(rng, E, t)
+            hip.step(a)
+            ora.step(a)
+            d = _same_words(hip.state(), ora.state, V)
+            assert d is None, f"step {t}: {d}"
+    finally:
+        hip.close()
+
+
 @pytest.mark.parametrize("E,N,order,pe,d", [(4096, None, "sorted", _abi.PE_NONE, 0),
                                             (16384, 30, "shuffled", _abi.PE_ROPE, 4)])
 def test_full_size_env_blocks_match_oracle(E, N, order, pe, d):
