@@ -106,6 +106,25 @@ struct SecProf {};
   do {                      \
   } while (0)
 #endif
+// Development builds (make prof / make waves -> libhwy_waves.so, tools/probe_waves.py):
+#if defined(HWY_SECTION_PROFILE) || defined(HWY_WAVE_TIMES)
+// per-env (start, end, done | HW_ID << 8 | XCC_ID << 40) of the last step launch, first
+// HWY_NWT envs
+#define HWY_NWT 16384
+__device__ unsigned long long g_hwy_wave_t[5 * HWY_NWT];
+#define WAVE_T(e, lane, k, val)                                          \
+  do {                                                                   \
+    if ((lane) == 0 && (e) < HWY_NWT) g_hwy_wave_t[5 * (e) + (k)] = (val); \
+  } while (0)
+#define WAVE_HWID()                                                                  \
+  (((unsigned long long)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) << 8) |  \
+   ((unsigned long long)(__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xff) << 40))
+#else
+#define WAVE_T(e, lane, k, val) \
+  do {                          \
+  } while (0)
+#define WAVE_HWID() 0ull
+#endif
 
 // ------------------------------------------------------------------------- vehicle state
 struct Veh {
@@ -958,6 +977,8 @@ __global__ void __launch_bounds__(256, 4) hwy_step_kernel(StepParams P) {
 
   SecProf sp;
   SEC_START(sp);
+  WAVE_T(e, lane, 0, __builtin_amdgcn_s_memtime());
+  WAVE_T(e, lane, 3, __builtin_amdgcn_s_memrealtime());
   Veh v;
   load_veh(st, fstride, idx, lane, V, v);
   const uint32_t ew = (st + HWY_F_ENV * fstride)[idx];
@@ -1042,6 +1063,9 @@ __global__ void __launch_bounds__(256, 4) hwy_step_kernel(StepParams P) {
   store_env_words(st, fstride, idx, lane, step, episode, seed, rdlf(v.aacc, 0), rdlf(v.asteer, 0),
                   ep_return);
   SEC(sp, 14);
+  WAVE_T(e, lane, 1, __builtin_amdgcn_s_memtime());
+  WAVE_T(e, lane, 4, __builtin_amdgcn_s_memrealtime());
+  WAVE_T(e, lane, 2, (unsigned long long)done | WAVE_HWID());
   SEC_FLUSH(sp, lane);
 }
 
@@ -1174,6 +1198,13 @@ int hwy_launch_math(int op, const float* in, const float* in2, float* out, int n
 }
 }
 
+#if defined(HWY_SECTION_PROFILE) || defined(HWY_WAVE_TIMES)
+extern "C" int hwy_debug_wave_times(unsigned long long* out, int n) {
+  if (n > 5 * HWY_NWT) n = 5 * HWY_NWT;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hwy_wave_t), sizeof(unsigned long long) * n) ==
+                 hipSuccess ? 0 : -2;
+}
+#endif
 #ifdef HWY_SECTION_PROFILE
 // development build only: copy out (and optionally clear) the section clock totals
 extern "C" int hwy_debug_sections(unsigned long long* out, int reset) {
