@@ -39,6 +39,7 @@
 #define KP_HEADING (1.0f / 0.2f)
 #define KP_LATERAL (1.0f / 0.6f)
 #define MAX_STEERING (HM_PI_F / 3.0f)
+#define TAN_MAX_STEERING 1.7320509f  // tan(MAX_STEERING), correctly rounded
 #define ACC_MAX 6.0f
 #define COMFORT_ACC_MAX 3.0f
 #define DISTANCE_WANTED 10.0f
@@ -129,7 +130,9 @@ __device__ unsigned long long g_hwy_wave_t[5 * HWY_NWT];
 // ------------------------------------------------------------------------- vehicle state
 struct Veh {
   float x, y, h, spd, tsp, dlt, tmr, ix, iy;
-  float aacc, asteer;  // Vehicle.action (lane 0: the ego's dict, persists across frames)
+  // Vehicle.action.  asteer: lane 0 the ego's steering angle (persists across frames); the
+  // traffic lanes hold the TANGENT of their clipped steering angle (what kinematics uses)
+  float aacc, asteer;
   int ln, tl;
   bool crashed, imp, present;
 };
@@ -196,8 +199,10 @@ __device__ __forceinline__ float idm_acc(float ev_spd, float ev_tsp, float ev_x,
   return acc;
 }
 
-// ControlledVehicle.steering_control(target lane c)
-__device__ __forceinline__ float steering_control(float y, float h, float spd, int c) {
+// ControlledVehicle.steering_control(target lane c) clipped to +-MAX_STEERING, returned as its
+// tangent.  Closed form (DESIGN.md deviations; oracle steering_tan): with z the clipped sine of
+// the slip angle, tan(clip(atan(2 tan(asin z)))) = clip(2 z / sqrt((1 - z)(1 + z)), +-tan MAX).
+__device__ __forceinline__ float steering_tan(float y, float h, float spd, int c) {
   float lat = lane_lat(y, c);
   float lane_future_heading = 0.0f;
   float lateral_speed_command = -KP_LATERAL * lat;
@@ -205,10 +210,10 @@ __device__ __forceinline__ float steering_control(float y, float h, float spd, i
       hm_asinf(hm_clipf(lateral_speed_command / hm_not_zero(spd), -1.0f, 1.0f));
   float heading_ref = lane_future_heading + hm_clipf(heading_command, -HM_PIO4_F, HM_PIO4_F);
   float heading_rate_command = KP_HEADING * hm_wrap_to_pi(heading_ref - h);
-  float slip_angle = hm_asinf(
-      hm_clipf((VEH_LENGTH / 2.0f) / hm_not_zero(spd) * heading_rate_command, -1.0f, 1.0f));
-  float steering_angle = hm_atanf(2.0f * hm_tanf_sc(slip_angle));
-  return hm_clipf(steering_angle, -MAX_STEERING, MAX_STEERING);
+  const float z =
+      hm_clipf((VEH_LENGTH / 2.0f) / hm_not_zero(spd) * heading_rate_command, -1.0f, 1.0f);
+  const float t = 2.0f * (z / __builtin_sqrtf((1.0f - z) * (1.0f + z)));
+  return hm_clipf(t, -TAN_MAX_STEERING, TAN_MAX_STEERING);
 }
 
 // utils.are_polygons_intersecting on the two 5x2 m rectangles (a = lower road index), in the
@@ -229,10 +234,13 @@ __device__ __forceinline__ float interval_distance(float min_a, float max_a, flo
   return min_a < min_b ? min_b - max_a : min_a - max_b;
 }
 
-__device__ __forceinline__ void sat_collide(float xa, float ya, float ca, float sa, float dax,
-                                            float day, float xb, float yb, float cb, float sb,
-                                            float dbx, float dby, bool* inter_out, bool* will_out,
-                                            float* tx, float* ty) {
+// `active`: this lane holds a pair.  The wave stops once every active lane has broken out
+// (nothing changes for a lane after its break), which after a's own two normals is the usual
+// case: cars in adjacent lanes separate on v_a, cars in one lane on u_a.
+__device__ __forceinline__ void sat_collide(bool active, float xa, float ya, float ca, float sa,
+                                            float dax, float day, float xb, float yb, float cb,
+                                            float sb, float dbx, float dby, bool* inter_out,
+                                            bool* will_out, float* tx, float* ty) {
   const float cdx = xa - xb, cdy = ya - yb;
   const float ddx = dax - dbx, ddy = day - dby;
   bool inter = true, will = true;
@@ -270,6 +278,7 @@ __device__ __forceinline__ void sat_collide(float xa, float ya, float ca, float 
         axy = cd > 0.0f ? sy : -sy;
       }
     }
+    if ((e & 1) && e < 7 && !wave_any(active && (inter || will))) break;
   }
   *inter_out = inter;
   *will_out = will;
@@ -700,7 +709,7 @@ struct CollLds {
 
 // ------------------------------------------------------------------------- one frame
 // Road.act() then Road.step(dt) for the env of this wave (lane = vehicle).
-__device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, RoadOrder& ro,
+__device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, float tan_ego, RoadOrder& ro,
                            float& cos_h, float& sin_h, CollLds& cl, SecProf& sp) {
   const int lanes = C.lanes_count;
   const float limit = C.speed_limit;
@@ -813,8 +822,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, Road
   const float ft_x = shf(v.x, st_), ft_spd = shf(v.spd, st_), ft_c = shf(ch, st_),
               ft_s = shf(sh, st_);
   if (actor) {
-    float steer = steering_control(v.y, v.h, v.spd, v.tl);
-    steer = hm_clipf(steer, -MAX_STEERING, MAX_STEERING);
+    const float steer = steering_tan(v.y, v.h, v.spd, v.tl);
     float acc = self_a;
     if (need_t) {
       const float acc_t =
@@ -839,9 +847,13 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, Road
     } else if (v.spd < MIN_SPEED) {
       v.aacc = hm_maxf(v.aacc, 1.0f * (MIN_SPEED - v.spd));
     }
-    const float beta = hm_atanf(0.5f * hm_tanf_sc(v.asteer));
-    float sdir, cdir;
-    hm_sincosf(v.h + beta, &sdir, &cdir);
+    // beta = atan(tan(steering) / 2) in closed form (oracle vehicle_step): cos and sin of beta
+    // from u = tan(beta), cos / sin of h + beta by angle addition from the carried cos / sin h
+    const float u = 0.5f * ((lane == 0 && !v.crashed) ? tan_ego : v.asteer);
+    const float cb = 1.0f / __builtin_sqrtf(1.0f + u * u);
+    const float sb = u * cb;
+    const float cdir = ch * cb - sh * sb;
+    const float sdir = sh * cb + ch * sb;
     const float vx = v.spd * cdir;
     const float vy = v.spd * sdir;
     v.x = v.x + vx * dt;
@@ -852,7 +864,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, Road
       v.crashed = true;
       v.imp = false;
     }
-    v.h = v.h + v.spd * hm_sinf(beta) / (VEH_LENGTH / 2.0f) * dt;
+    v.h = v.h + v.spd * sb / (VEH_LENGTH / 2.0f) * dt;
     v.spd = v.spd + v.aacc * dt;
     v.ln = closest_lane(v.y, lanes);  // on_state_update
   }
@@ -935,7 +947,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, Road
     if (!wave_any(pass)) continue;
     bool inter, will;
     float tx, ty;
-    sat_collide(xa, ya, ca, sa, (va * ca) * dt, (va * sa) * dt, xb, yb, cb, sb, (vb * cb) * dt,
+    sat_collide(pass, xa, ya, ca, sa, (va * ca) * dt, (va * sa) * dt, xb, yb, cb, sb, (vb * cb) * dt,
                 (vb * sb) * dt, &inter, &will, &tx, &ty);
     if (pass && will) {
       atomicMax(&cl.imx[a], ((uint64_t)(b + 1) << 32) | hm_f2bits(tx / 2.0f));
@@ -1002,13 +1014,14 @@ __global__ void __launch_bounds__(256, 4) hwy_step_kernel(StepParams P) {
   float cos_h, sin_h;
   hm_sincosf(v.h, &sin_h, &cos_h);
   SEC(sp, 15);
-  for (int frame = 0; frame < frames; ++frame) {
-    if (frame == 0 && lane == 0) {  // ContinuousAction.act
-      v.aacc = hm_lmap(hm_clipf(a0, -1.0f, 1.0f), -1.0f, 1.0f, -5.0f, 5.0f);
-      v.asteer = hm_lmap(hm_clipf(a1, -1.0f, 1.0f), -1.0f, 1.0f, -HM_PIO4_F, HM_PIO4_F);
-    }
-    frame_wave(C, lane, v, dt, ro, cos_h, sin_h, lds_coll[w], sp);
+  if (frames > 0 && lane == 0) {  // ContinuousAction.act (first frame)
+    v.aacc = hm_lmap(hm_clipf(a0, -1.0f, 1.0f), -1.0f, 1.0f, -5.0f, 5.0f);
+    v.asteer = hm_lmap(hm_clipf(a1, -1.0f, 1.0f), -1.0f, 1.0f, -HM_PIO4_F, HM_PIO4_F);
   }
+  // the ego's steering changes only here and to 0 on a crash (handled in frame_wave)
+  const float tan_ego = rdlf(lane == 0 ? hm_tanf_sc(v.asteer) : 0.0f, 0);
+  for (int frame = 0; frame < frames; ++frame)
+    frame_wave(C, lane, v, dt, tan_ego, ro, cos_h, sin_h, lds_coll[w], sp);
   step += 1;
   SEC(sp, 11);
 

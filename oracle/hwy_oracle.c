@@ -42,6 +42,7 @@
 #define KP_HEADING (1.0f / 0.2f) /* 1/TAU_HEADING */
 #define KP_LATERAL (1.0f / 0.6f) /* 1/TAU_LATERAL */
 #define MAX_STEERING (HM_PI_F / 3.0f)
+#define TAN_MAX_STEERING 1.7320509f /* tan(MAX_STEERING), correctly rounded */
 #define ACC_MAX 6.0f             /* IDMVehicle.ACC_MAX */
 #define COMFORT_ACC_MAX 3.0f
 #define COMFORT_ACC_MIN (-5.0f)
@@ -63,6 +64,7 @@ typedef struct {
   int lane, target_lane;
   int crashed, present;
   float act_steer, act_acc; /* Vehicle.action dict */
+  float act_tan;             /* traffic: tan of the clipped steering (steering_tan) */
 } Veh;
 
 typedef struct {
@@ -103,6 +105,7 @@ static void load_road(Road* r, const hwy_config* cfg, uint32_t* st, int E, int e
     v->present = (fl & HWY_FLAG_PRESENT) != 0;
     v->act_steer = 0.0f;
     v->act_acc = 0.0f;
+    v->act_tan = 0.0f;
   }
   uint32_t* ew = fld(st, HWY_F_ENV, E, e);
   r->step = (int)ew[HWY_E_STEP];
@@ -285,9 +288,9 @@ static void change_lane_policy(Road* r, int self) {
   }
 }
 
-/* ControlledVehicle.steering_control(target_lane_index) */
-static float steering_control(const Road* r, int self, int c) {
-  const Veh* me = &r->v[self];
+/* ControlledVehicle.steering_control(target_lane_index), transliterated (kept as the check of
+ * steering_tan below: hwyo_kin_compare / tests/test_oracle_env.py) */
+static float steering_control_v(const Veh* me, int c) {
   float lat = lane_lat(me->y, c);
   float lane_future_heading = 0.0f;
   float lateral_speed_command = -KP_LATERAL * lat;
@@ -299,13 +302,28 @@ static float steering_control(const Road* r, int self, int c) {
   return hm_clipf(steering_angle, -MAX_STEERING, MAX_STEERING);
 }
 
+/* The same steering, clipped to +-MAX_STEERING, as the tangent kinematics needs (DESIGN.md
+ * deviations).  With z the clipped sine of the slip angle:
+ * tan(clip(atan(2 tan(asin z)))) = clip(2 z / sqrt((1 - z)(1 + z)), +-tan MAX_STEERING).
+ * The kernel's steering_tan is this expression. */
+static float steering_tan_v(const Veh* me, int c) {
+  float lat = lane_lat(me->y, c);
+  float lane_future_heading = 0.0f;
+  float lateral_speed_command = -KP_LATERAL * lat;
+  float heading_command = hm_asinf(hm_clipf(lateral_speed_command / hm_not_zero(me->speed), -1.0f, 1.0f));
+  float heading_ref = lane_future_heading + hm_clipf(heading_command, -HM_PIO4_F, HM_PIO4_F);
+  float heading_rate_command = KP_HEADING * hm_wrap_to_pi(heading_ref - me->heading);
+  float z = hm_clipf((VEH_LENGTH / 2.0f) / hm_not_zero(me->speed) * heading_rate_command, -1.0f, 1.0f);
+  float t = 2.0f * (z / sqrtf((1.0f - z) * (1.0f + z)));
+  return hm_clipf(t, -TAN_MAX_STEERING, TAN_MAX_STEERING);
+}
+
 /* IDMVehicle.act */
 static void idm_act(Road* r, int self) {
   Veh* me = &r->v[self];
   if (me->crashed) return;
   change_lane_policy(r, self);
-  float steer = steering_control(r, self, me->target_lane);
-  steer = hm_clipf(steer, -MAX_STEERING, MAX_STEERING);
+  float steer_tan = steering_tan_v(me, me->target_lane);
   int front, rear;
   neighbour_vehicles(r, self, me->lane, &front, &rear);
   float acc = idm_acceleration(r, self, self, front);
@@ -315,7 +333,7 @@ static void idm_act(Road* r, int self) {
     acc = hm_minf(acc, target_idm_acceleration);
   }
   acc = hm_clipf(acc, -ACC_MAX, ACC_MAX);
-  me->act_steer = steer;
+  me->act_tan = steer_tan;
   me->act_acc = acc;
 }
 
@@ -327,6 +345,7 @@ static void vehicle_step(Road* r, int i) {
   /* clip_actions */
   if (v->crashed) {
     v->act_steer = 0.0f;
+    v->act_tan = 0.0f;
     v->act_acc = -1.0f * v->speed;
   }
   if (v->speed > MAX_SPEED) {
@@ -334,10 +353,17 @@ static void vehicle_step(Road* r, int i) {
   } else if (v->speed < MIN_SPEED) {
     v->act_acc = hm_maxf(v->act_acc, 1.0f * (MIN_SPEED - v->speed));
   }
-  float delta_f = v->act_steer;
-  float beta = hm_atanf(0.5f * hm_tanf(delta_f));
-  float vx = v->speed * hm_cosf(v->heading + beta);
-  float vy = v->speed * hm_sinf(v->heading + beta);
+  /* beta = atan(tan(delta_f) / 2), delta_f = the steering angle; in closed form (DESIGN.md
+   * deviations): cos beta = 1 / sqrt(1 + u^2), sin beta = u cos beta with u = tan(delta_f) / 2,
+   * and cos / sin of heading + beta by angle addition.  The ego's tangent is taken from its
+   * angle; the traffic's comes from steering_tan.  kinematics_upstream is the transliteration. */
+  float tan_delta = i == 0 ? hm_tanf(v->act_steer) : v->act_tan;
+  float u = 0.5f * tan_delta;
+  float cbeta = 1.0f / sqrtf(1.0f + u * u);
+  float sbeta = u * cbeta;
+  float ch = hm_cosf(v->heading), sh = hm_sinf(v->heading);
+  float vx = v->speed * (ch * cbeta - sh * sbeta);
+  float vy = v->speed * (sh * cbeta + ch * sbeta);
   v->x = v->x + vx * dt;
   v->y = v->y + vy * dt;
   if (v->has_impact) {
@@ -346,7 +372,7 @@ static void vehicle_step(Road* r, int i) {
     v->crashed = 1;
     v->has_impact = 0;
   }
-  v->heading = v->heading + v->speed * hm_sinf(beta) / (VEH_LENGTH / 2.0f) * dt;
+  v->heading = v->heading + v->speed * sbeta / (VEH_LENGTH / 2.0f) * dt;
   v->speed = v->speed + v->act_acc * dt;
   v->lane = closest_lane(v->y, r->cfg->lanes_count); /* on_state_update */
 }
@@ -502,6 +528,43 @@ static void rect_sat(float xa, float ya, float ca, float sa, float dax, float da
 
 /* Both forms on the same pairs (test hook).  in[n][12] = xa ya ha spa xb yb hb spb dt (3 unused);
  * out[n][8] = polygon form (inter, will, tx, ty), closed form (inter, will, tx, ty). */
+/* Steering and kinematics: upstream's angle form against the closed forms the simulation uses.
+ * in[i] = (y, heading, speed, target lane, ego steering angle); out[i] = (upstream tan of the
+ * clipped steering, steering_tan, then for the ego angle and for the traffic steering: vx, vy,
+ * heading rate by upstream's kinematics and by the closed form = 12 values). */
+static void kin_upstream(float h, float spd, float delta, float* vx, float* vy, float* hr) {
+  float beta = hm_atanf(0.5f * hm_tanf(delta));
+  *vx = spd * hm_cosf(h + beta);
+  *vy = spd * hm_sinf(h + beta);
+  *hr = spd * hm_sinf(beta) / (VEH_LENGTH / 2.0f);
+}
+static void kin_closed(float h, float spd, float tan_delta, float* vx, float* vy, float* hr) {
+  float u = 0.5f * tan_delta;
+  float cbeta = 1.0f / sqrtf(1.0f + u * u);
+  float sbeta = u * cbeta;
+  float ch = hm_cosf(h), sh = hm_sinf(h);
+  *vx = spd * (ch * cbeta - sh * sbeta);
+  *vy = spd * (sh * cbeta + ch * sbeta);
+  *hr = spd * sbeta / (VEH_LENGTH / 2.0f);
+}
+int hwyo_kin_compare(const float* in, int n, float* out) {
+  for (int i = 0; i < n; ++i) {
+    const float* p = in + 5 * i;
+    float* o = out + 14 * i;
+    Veh v = {0};
+    v.y = p[0], v.heading = p[1], v.speed = p[2];
+    const int c = (int)p[3];
+    const float steer = steering_control_v(&v, c);
+    o[0] = hm_tanf(steer);
+    o[1] = steering_tan_v(&v, c);
+    kin_upstream(v.heading, v.speed, p[4], &o[2], &o[3], &o[4]);
+    kin_closed(v.heading, v.speed, hm_tanf(p[4]), &o[5], &o[6], &o[7]);
+    kin_upstream(v.heading, v.speed, steer, &o[8], &o[9], &o[10]);
+    kin_closed(v.heading, v.speed, o[1], &o[11], &o[12], &o[13]);
+  }
+  return 0;
+}
+
 int hwyo_sat_compare(const float* in, int n, float* out) {
   for (int i = 0; i < n; ++i) {
     const float* p = in + 12 * i;

@@ -69,6 +69,7 @@ def lib():
         L.hwyo_philox.argtypes = [_u32p, _u32p, _u32p]
         L.hwyo_philox.restype = None
         L.hwyo_sat_compare.argtypes = [_f32p, ctypes.c_int, _f32p]
+        L.hwyo_kin_compare.argtypes = [_f32p, ctypes.c_int, _f32p]
         _lib = L
     return _lib
 
@@ -163,6 +164,16 @@ def sat_compare(pairs: np.ndarray) -> np.ndarray:
     p = np.ascontiguousarray(pairs, np.float32)
     out = np.zeros((p.shape[0], 8), np.float32)
     assert lib().hwyo_sat_compare(p, p.shape[0], out) == 0
+    return out
+
+
+def kin_compare(rows: np.ndarray) -> np.ndarray:
+    """[n, 5] (y, heading, speed, target lane, ego steering) -> [n, 14]: upstream tan of the
+    clipped steering, the closed-form steering_tan; (vx, vy, heading rate) upstream / closed
+    form for the ego angle, then for the traffic steering."""
+    p = np.ascontiguousarray(rows, np.float32)
+    out = np.zeros((p.shape[0], 14), np.float32)
+    assert lib().hwyo_kin_compare(p, p.shape[0], out) == 0
     return out
 
 

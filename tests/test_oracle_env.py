@@ -167,3 +167,47 @@ def test_rectangle_sat_closed_form_matches_polygon_sat():
     mag = np.linalg.norm(o[both, 2:4], axis=1)
     assert np.mean(d <= 2e-4) > 0.999
     assert np.all(d <= 3e-4 + 5e-3 * mag)
+
+
+def _steering_f64(y, h, spd, c):
+    """ControlledVehicle.steering_control in float64 (upstream's own precision)."""
+    y, h, spd = (np.asarray(a, np.float64) for a in (y, h, spd))
+    lat = y - c * 4.0
+    nz = np.where(np.abs(spd) > 1e-2, spd, np.where(spd >= 0, 1e-2, -1e-2))
+    hc = np.arcsin(np.clip(-(1 / 0.6) * lat / nz, -1, 1))
+    href = np.clip(hc, -np.pi / 4, np.pi / 4)
+    hrc = (1 / 0.2) * (((href - h + np.pi) % (2 * np.pi)) - np.pi)
+    slip = np.arcsin(np.clip(5.0 / 2 / nz * hrc, -1, 1))
+    return np.clip(np.arctan(2 * np.tan(slip)), -np.pi / 3, np.pi / 3)
+
+
+def test_closed_form_steering_and_kinematics_match_upstream_forms():
+    """steering_tan and the closed-form bicycle kinematics (oracle vehicle_step, mirrored by the
+    kernel) against upstream's angle forms: in float64, and transliterated in binary32."""
+    rng = np.random.default_rng(5)
+    n = 200000
+    p = np.zeros((n, 5), np.float32)
+    p[:, 0] = rng.uniform(-3, 15, n)          # y
+    p[:, 1] = rng.normal(0, 0.2, n)           # heading
+    p[:, 2] = rng.uniform(-5, 40, n)          # speed (incl. slow cars: large slip commands)
+    p[:, 3] = rng.integers(0, 4, n)           # target lane
+    p[:, 4] = rng.uniform(-np.pi / 4, np.pi / 4, n)  # ego steering angle
+    o = oracle.kin_compare(p).astype(np.float64)
+    t64 = np.tan(_steering_f64(p[:, 0], p[:, 1], p[:, 2], p[:, 3]))
+    t_up, t_cf = o[:, 0], o[:, 1]
+    assert np.mean(np.abs(t64) >= 1.7320) > 0.05  # the clip is exercised
+    # the closed form follows float64 upstream to the binary32 rounding of its inputs (small
+    # tangents come from cancelling heading differences: absolute floor)
+    tol = 2e-6 + 2e-5 * np.abs(t64)
+    assert np.all(np.abs(t_cf - t64) <= tol)
+    # the binary32 angle form agrees with it, except where the slip command saturates (|z| = 1):
+    # tan(float(pi/2)) is negative in binary32, which flips that steering to the opposite clip
+    bad = np.abs(t_up - t_cf) > 1e-6 + 2e-6 * np.abs(t_cf)
+    assert np.all(np.abs(t_up[bad] + t64[bad]) <= 1e-5 * np.abs(t64[bad]))
+    assert np.all(np.abs(np.abs(t64[bad]) - np.sqrt(3.0)) < 1e-5)
+    # kinematics (vx, vy, heading rate), closed form vs angle form, for the ego angle and for the
+    # traffic steering where both steering forms agree
+    scale = np.abs(p[:, 2:3]).astype(np.float64) + 1e-3
+    assert np.all(np.abs(o[:, 5:8] - o[:, 2:5]) <= 1e-6 * scale)
+    ok = ~bad
+    assert np.all(np.abs(o[ok, 11:14] - o[ok, 8:11]) <= 4e-6 * scale[ok])
