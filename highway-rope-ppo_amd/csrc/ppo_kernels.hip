@@ -328,6 +328,37 @@ __global__ void __launch_bounds__(256) gemm64v(GemmArgs g) {
   if (do_colsum && m0 + t < g.M) g.bias_part[(long)blockIdx.z * g.M + m0 + t] = colsum;
 }
 
+// Tile image of the row kernels' weights (in the workspace): for a matrix read as B[k][n] in
+// 16-deep k blocks, tile (G, b) is the 1-KB MFMA operand of columns 16G..16G+15 and block b:
+// float 4*(16g + c) + j = B[16b + 4g + j][16G + c] (0 past K), tiles ordered G-major.  Forward
+// images (f*) hold B = W^T of W1, W2, Wa1, Wc1; backward images (b*) B = W of Wa1, Wc1, W2.
+struct TileGeom {
+  int64_t f1, f2, fa, fc, ba, bc, b2, total;  // float offsets
+};
+__host__ __device__ inline TileGeom tile_geom(int S, int H, int sb, int hb) {
+  TileGeom T;
+  const int64_t g = H / 16, big = g * hb * 256;
+  T.f1 = 0;
+  T.f2 = g * sb * 256;
+  T.fa = T.f2 + big;
+  T.fc = T.fa + big;
+  T.ba = T.fc + big;
+  T.bc = T.ba + big;
+  T.b2 = T.bc + big;
+  T.total = T.b2 + big;
+  return T;
+}
+// ring depth of the row kernels for H (ppo_rows<H/64, NW>: 16-column tiles per wave TW)
+__host__ __device__ inline int rows_ring_depth(int H) {
+  const int qh = H / 64, nw = (qh % 2 == 0) ? 8 : 4, tw = H / nw / 16;
+  return tw <= 4 ? 4 : 2;
+}
+__host__ __device__ inline void rows_blocks(int S, int H, int* sb, int* hb) {
+  const int D = rows_ring_depth(H);
+  *hb = (H / 16 + D - 1) / D * D;
+  *sb = ((S + 15) / 16 + D - 1) / D * D;
+}
+
 // ----------------------------------------------------------------------------- layout
 struct Layout {
   int64_t off[13];
@@ -368,10 +399,12 @@ struct Work {
   float *norm_part;          // [max(nred, nred2)]
   float *wg_slab;            // fused: [ntile][split][64*64 + 64] partial tiles
   float *xg;                 // fused: [B][S] gathered states
+  float *wtile;              // fused: weight tile image (TileGeom)
   int nhead, HP, sa, s2, s1, ca, c2, c1, nred;
   // fused path (ppo_rows + ppo_wgrad)
   bool fused;
   int n1, tac, t2, t1, nh, split, grid2, nred2;
+  int sb, hb;  // ring blocks of the row kernels (rows_blocks)
 };
 
 // the fused row path covers the reference's shapes: float4 state rows, H a multiple of 64
@@ -418,17 +451,19 @@ inline Work carve(const hwy_ppo_dims& d, void* ws, int64_t* bytes_out) {
   const int64_t sa = w.fused ? 0 : w.sa, s2 = w.fused ? 0 : w.s2, s1 = w.fused ? 0 : w.s1;
   const int64_t wg_slab_n = w.fused ? (int64_t)ntile * w.split * (64 * 64 + 64) : 0;
   const int64_t xg_n = w.fused ? (int64_t)B * S : 0;
-  int64_t sizes[16] = {
+  rows_blocks(S, H, &w.sb, &w.hb);
+  const int64_t tile_n = w.fused ? tile_geom(S, H, w.sb, w.hb).total : 0;
+  int64_t sizes[17] = {
       (int64_t)B * H, (int64_t)B * H, (int64_t)B * 2 * H, (int64_t)B * 2 * H, (int64_t)B * H,
       (int64_t)B * H, head_rows * w.HP, sa * 2 * H * H, sa * 2 * H,
       s2 * H * H, s2 * H, s1 * H * S, s1 * H,
-      norm_n, wg_slab_n, xg_n};
+      norm_n, wg_slab_n, xg_n, tile_n};
   float* p = (float*)ws;
-  float** dst[16] = {&w.h1, &w.h2, &w.ac, &w.dac, &w.dh2, &w.dh1, &w.head_part, &w.slab_ac,
+  float** dst[17] = {&w.h1, &w.h2, &w.ac, &w.dac, &w.dh2, &w.dh1, &w.head_part, &w.slab_ac,
                      &w.bias_ac, &w.slab_2, &w.bias_2, &w.slab_1, &w.bias_1, &w.norm_part,
-                     &w.wg_slab, &w.xg};
+                     &w.wg_slab, &w.xg, &w.wtile};
   int64_t total = 0;
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < 17; ++i) {
     int64_t n = (sizes[i] + 63) / 64 * 64;  // 256-B aligned sub-buffers
     if (p) *dst[i] = p + total;
     total += n;
@@ -601,6 +636,7 @@ struct RowArgs {
   int64_t off[13];
   float *h1, *h2, *dac, *dh2, *dh1;
   float* xg;         // [B][S] gathered states (ppo_wgrad's dW1 operand)
+  const float* tiles;  // weight tile image (TileGeom), in sync with params
   float* head_part;  // [gridDim.x][HP]
   int HP;
   float eps_clip, value_coef, entropy_coef;
@@ -619,10 +655,10 @@ __device__ __forceinline__ int row_pitch(int n) { return n + 4; }  // n/4 + 1 od
 
 struct WSeg {
   const float* W;
-  int ldw, K, nblk, nn;  // nn: W is [K][N] (k-major), else [N][K]
+  int ldw, K, nblk, nn;  // nn: 0 W is [N][K], 1 W is [K][N] (k-major), 2 W is a tile image
 };
 
-template <int TW, int D, int NSEG>
+template <int TW, int D, int NSEG, bool TL>
 struct WRing {
   f32x4 buf[D][TW];
   WSeg sg[NSEG];
@@ -633,6 +669,13 @@ struct WRing {
   // clamped into range here and zeroed when the block is consumed.
   __device__ __forceinline__ void load_blk(const float* W, int ldw, int nn, int kb,
                                            f32x4 (&dst)[TW]) {
+    if constexpr (TL) {  // tile image (TileGeom): one contiguous KB per 16 columns and block
+      const float* p = W + ((long)(n_base / 16) * ldw + (kb >> 4)) * 256 + (16 * g + c) * 4;
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+        dst[t] = *reinterpret_cast<const f32x4*>(p + (long)t * ldw * 256);
+      return;
+    }
     const int k = kb + 4 * g;
     const long sn = nn ? 1 : ldw, sk = nn ? ldw : 1;
 #pragma unroll
@@ -699,16 +742,28 @@ template <int TW>
 constexpr int ring_depth() { return TW <= 2 ? 4 : (TW <= 4 ? 4 : 2); }
 
 // segment table of the row kernels: forward W1, W2, Wa1, Wc1 ([N][K]); backward Wa1, Wc1, W2
-// read k-major for dh2 = dac [Wa1; Wc1] and dh1 = dh2 W2
-template <int TW, int D, int NSEG>
-__device__ __forceinline__ void ring_setup(WRing<TW, D, NSEG>& R, const float* P, const int64_t* off,
-                                           int S, int H, int n_base) {
+// read k-major for dh2 = dac [Wa1; Wc1] and dh1 = dh2 W2.  With a tile image (TileGeom; kept by
+// hwy_ppo_sync_params / ppo_adam) every segment streams whole 1-KB tiles instead.
+template <int TW, int D, int NSEG, bool TL>
+__device__ __forceinline__ void ring_setup(WRing<TW, D, NSEG, TL>& R, const float* P,
+                                           const int64_t* off, int S, int H, int n_base,
+                                           const float* tiles) {
   const int lane = threadIdx.x & 63;
   R.g = lane >> 4;
   R.c = lane & 15;
   R.n_base = n_base;
   const int hb = (H / 16 + D - 1) / D * D;
   const int sb = ((S + 15) / 16 + D - 1) / D * D;
+  if constexpr (TL) {
+    const TileGeom T = tile_geom(S, H, sb, hb);
+    const WSeg all[7] = {{tiles + T.f1, sb, 16 * sb, sb, 2},  {tiles + T.f2, hb, H, hb, 2},
+                         {tiles + T.fa, hb, H, hb, 2},        {tiles + T.fc, hb, H, hb, 2},
+                         {tiles + T.ba, hb, H, hb, 2},        {tiles + T.bc, hb, H, hb, 2},
+                         {tiles + T.b2, hb, H, hb, 2}};
+#pragma unroll
+    for (int i = 0; i < NSEG; ++i) R.sg[i] = all[i];
+    return;
+  }
   const WSeg all[7] = {{P + off[P_W1], S, S, sb, 0},   {P + off[P_W2], H, H, hb, 0},
                        {P + off[P_WA1], H, H, hb, 0},  {P + off[P_WC1], H, H, hb, 0},
                        {P + off[P_WA1], H, H, hb, 1},  {P + off[P_WC1], H, H, hb, 1},
@@ -759,8 +814,8 @@ __device__ __forceinline__ void row_epi_mask(const f32x4 (&acc)[QH], float* mask
 // Forward of the 16 rows starting at row0 (rows idx[row0 + i], or row0 + i without idx) into
 // the LDS images X, H1, H2, AC = [a1 | c1]; optionally also to HBM (xg, h1, h2; null = no).
 // Ends with a workgroup barrier.
-template <int QH, int NW, int D, int NSEG>
-__device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG>& R, const float* states,
+template <int QH, int NW, int D, int NSEG, bool TL>
+__device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG, TL>& R, const float* states,
                                              const int64_t* idx, int S, int nrows, int row0,
                                              const float* P, const int64_t* off, float* X,
                                              float* H1, float* H2, float* AC, float* xg,
@@ -832,8 +887,8 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   const int nrows = min(kRowTile, r.B - row0);
   const float* P = r.params;
   constexpr int D = ring_depth<TW>();
-  WRing<TW, D, 7> R;
-  ring_setup(R, P, r.off, S, H, w * (H / NW));
+  WRing<TW, D, 7, true> R;
+  ring_setup(R, P, r.off, S, H, w * (H / NW), r.tiles);
   R.prime();
   rows_forward<QH, NW>(R, r.states, r.idx, S, nrows, row0, P, r.off, X, H1, H2, AC, r.xg, r.h1,
                        r.h2 PSEC_ARGS);
@@ -1001,8 +1056,8 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_act(ActArgs r) {
   const float* P = r.params;
   constexpr int TW = H_TW(QH, NW);
   constexpr int D = ring_depth<TW>();
-  WRing<TW, D, 4> R;
-  ring_setup(R, P, r.off, r.S, H, w * (H / NW));
+  WRing<TW, D, 4, false> R;
+  ring_setup(R, P, r.off, r.S, H, w * (H / NW), nullptr);
   R.prime();
 #ifdef HWY_SECTION_PROFILE
   uint64_t _pt = 0, _pacc[16];
@@ -1412,7 +1467,77 @@ struct OptArgs {
   int64_t numel;
   const int32_t* counters;
   float lr, beta1, beta2, eps, max_norm;
+  float* tiles;  // fused path: the weight tile image, rewritten with the new weights
+  int64_t o_w1, o_w2, o_wa1, o_wc1;
+  int S, H, sb, hb;
 };
+
+// float index of B[k][n] in a tile image region with nblk blocks per 16 columns
+__device__ __forceinline__ int64_t tile_index(int k, int n, int nblk) {
+  return ((int64_t)(n >> 4) * nblk + (k >> 4)) * 256 + ((((k & 15) >> 2) << 4) + (n & 15)) * 4 +
+         (k & 3);
+}
+
+// the tile image entries of flat parameter i (new value v)
+__device__ __forceinline__ void write_tiles(const OptArgs& o, int64_t i, float v) {
+  const TileGeom T = tile_geom(o.S, o.H, o.sb, o.hb);
+  const int64_t H = o.H;
+  int64_t j = i - o.o_w1;
+  if (j >= 0 && j < H * o.S) {  // W1 [H][S]: forward only, B[k][n] = W1[n][k]
+    const int n = (int)(j / o.S), k = (int)(j - (int64_t)n * o.S);
+    o.tiles[T.f1 + tile_index(k, n, o.sb)] = v;
+    return;
+  }
+  const int64_t offs[3] = {o.o_w2, o.o_wa1, o.o_wc1};
+  const int64_t fwd[3] = {T.f2, T.fa, T.fc}, bwd[3] = {T.b2, T.ba, T.bc};
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    j = i - offs[q];
+    if (j >= 0 && j < H * H) {  // [H][H]: forward B = W^T, backward B = W
+      const int n = (int)(j / H), k = (int)(j - (int64_t)n * H);
+      o.tiles[fwd[q] + tile_index(k, n, o.hb)] = v;
+      o.tiles[bwd[q] + tile_index(n, k, o.hb)] = v;
+      return;
+    }
+  }
+}
+
+struct TileArgs {
+  const float* P;
+  int64_t o_w1, o_w2, o_wa1, o_wc1;
+  int S, H, sb, hb;
+  float* tiles;
+};
+
+// the whole tile image from params (hwy_ppo_sync_params): one float per thread
+__global__ void __launch_bounds__(256) ppo_retile(TileArgs a) {
+  const TileGeom T = tile_geom(a.S, a.H, a.sb, a.hb);
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= T.total) return;
+  const float* W;
+  int64_t base;
+  int K, nblk;
+  bool fwd;
+  if (i < T.f2) W = a.P + a.o_w1, base = T.f1, K = a.S, nblk = a.sb, fwd = true;
+  else if (i < T.fa) W = a.P + a.o_w2, base = T.f2, K = a.H, nblk = a.hb, fwd = true;
+  else if (i < T.fc) W = a.P + a.o_wa1, base = T.fa, K = a.H, nblk = a.hb, fwd = true;
+  else if (i < T.ba) W = a.P + a.o_wc1, base = T.fc, K = a.H, nblk = a.hb, fwd = true;
+  else if (i < T.bc) W = a.P + a.o_wa1, base = T.ba, K = a.H, nblk = a.hb, fwd = false;
+  else if (i < T.b2) W = a.P + a.o_wc1, base = T.bc, K = a.H, nblk = a.hb, fwd = false;
+  else W = a.P + a.o_w2, base = T.b2, K = a.H, nblk = a.hb, fwd = false;
+  const int64_t r = i - base;
+  const int tile = (int)(r >> 8), e = (int)(r & 255);
+  const int G = tile / nblk, b = tile - G * nblk;
+  const int l = e >> 2, jj = e & 3;
+  const int k = 16 * b + 4 * (l >> 4) + jj, n = 16 * G + (l & 15);
+  float v = 0.0f;
+  if (fwd) {
+    if (k < K) v = W[(int64_t)n * K + k];  // B[k][n] = W[n][k], W [H][K]
+  } else {
+    if (k < a.H) v = W[(int64_t)k * a.H + n];  // B[k][n] = W[k][n], W [H][H]
+  }
+  a.tiles[i] = v;
+}
 
 // sum of squares of the (all-reduced) gradient, same partition as ppo_reduce
 __global__ void __launch_bounds__(kRedThreads) ppo_sumsq(const float* g, int64_t n, float* part) {
@@ -1461,7 +1586,9 @@ __global__ void __launch_bounds__(256) ppo_adam(OptArgs o) {
   o.m[i] = mm;
   o.v[i] = vv;
   const float denom = sqrtf(vv) / bc2_sqrt + o.eps;
-  o.params[i] = o.params[i] - step_size * (mm / denom);
+  const float pn = o.params[i] - step_size * (mm / denom);
+  o.params[i] = pn;
+  if (o.tiles) write_tiles(o, i, pn);
 }
 
 template <int AM, int BM, int EPI>
@@ -1522,6 +1649,7 @@ int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
     r.adv = a->adv, r.ret = a->ret, r.params = P;
     for (int i = 0; i < 13; ++i) r.off[i] = L.off[i];
     r.h1 = w.h1, r.h2 = w.h2, r.dac = w.dac, r.dh2 = w.dh2, r.dh1 = w.dh1, r.xg = w.xg;
+    r.tiles = w.wtile;
     r.head_part = w.head_part, r.HP = w.HP;
     r.eps_clip = a->eps_clip, r.value_coef = a->value_coef, r.entropy_coef = a->entropy_coef;
     r.counters = a->counters;
@@ -1689,7 +1817,30 @@ int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream) {
   o.nred = (w.fused && !a->grads_modified) ? w.nred2 : w.nred;
   o.lr = a->lr, o.beta1 = a->beta1, o.beta2 = a->beta2, o.eps = a->adam_eps;
   o.max_norm = a->max_grad_norm;
+  if (w.fused) {
+    o.tiles = w.wtile;
+    o.o_w1 = L.off[P_W1], o.o_w2 = L.off[P_W2], o.o_wa1 = L.off[P_WA1], o.o_wc1 = L.off[P_WC1];
+    o.S = d.S, o.H = d.H, o.sb = w.sb, o.hb = w.hb;
+  }
   hipLaunchKernelGGL(ppo_adam, dim3(w.nred), dim3(256), 0, s, o);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int hwy_ppo_sync_params(const hwy_ppo_args* a, void* stream) {
+  if (!a || !a->params || !a->workspace) return -1;
+  const hwy_ppo_dims& d = a->dims;
+  if (hwy_ppo_workspace_bytes(&d) < 0) return -1;
+  Work w = carve(d, a->workspace, nullptr);
+  if (!w.fused) return 0;  // the general path reads params directly
+  const Layout L = make_layout(d);
+  TileArgs t = {};
+  t.P = a->params;
+  t.o_w1 = L.off[P_W1], t.o_w2 = L.off[P_W2], t.o_wa1 = L.off[P_WA1], t.o_wc1 = L.off[P_WC1];
+  t.S = d.S, t.H = d.H, t.sb = w.sb, t.hb = w.hb;
+  t.tiles = w.wtile;
+  const int64_t n = tile_geom(d.S, d.H, w.sb, w.hb).total;
+  hipLaunchKernelGGL(ppo_retile, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, t);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -65,6 +65,8 @@ def _bind(L):
     L.hwy_ppo_forward_backward.restype = ctypes.c_int
     L.hwy_ppo_optimizer.argtypes = [ctypes.POINTER(PpoArgs), ctypes.c_void_p]
     L.hwy_ppo_optimizer.restype = ctypes.c_int
+    L.hwy_ppo_sync_params.argtypes = [ctypes.POINTER(PpoArgs), ctypes.c_void_p]
+    L.hwy_ppo_sync_params.restype = ctypes.c_int
     L.hwy_ppo_act.argtypes = [ctypes.POINTER(PpoActArgs), ctypes.c_void_p]
     L.hwy_ppo_act.restype = ctypes.c_int
     L._ppo_bound = True
@@ -232,6 +234,11 @@ class FusedPPO:
     def _opt(self, a):
         check(self.L.hwy_ppo_optimizer(ctypes.byref(a), stream_ptr()), "hwy_ppo_optimizer")
 
+    def sync_params(self, a):
+        """Rebuild the workspace's weight tile image from the flat params (hwy_ppo_sync_params);
+        needed before a step whenever params changed outside hwy_ppo_optimizer."""
+        check(self.L.hwy_ppo_sync_params(ctypes.byref(a), stream_ptr()), "hwy_ppo_sync_params")
+
     def _allreduce(self):
         if self._avg_op:  # RCCL averages in the collective (no extra division kernel)
             torch.distributed.all_reduce(self.grads, op=torch.distributed.ReduceOp.AVG,
@@ -248,6 +255,9 @@ class FusedPPO:
         args = [self._args(states, pre_tanh, old_lp, adv, ret, perm.data_ptr() + i * mb * 8)
                 for i in range(nmb)]
         self.counters[1].zero_()
+        # the weight tile image the row kernel streams: params may have been written since the
+        # last update (checkpoint load, torch optimizer); hwy_ppo_optimizer keeps it in step
+        self.sync_params(args[0])
         if not self.use_graphs:
             for _ in range(epochs):
                 for a in args:

@@ -13,8 +13,14 @@
  *   actor_mean.2.{weight,bias} log_std critic.0.{weight,bias} critic.2.{weight,bias}
  * (weights [out, in] row-major, as nn.Linear stores them).
  *
- * All math is fp32; GEMMs use v_mfma_f32_32x32x2_f32 (exact fp32 products, fp32 accumulate).
+ * All math is fp32; GEMMs use v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulate).
  * Calls are asynchronous, allocate nothing and are hipGraph-capturable.
+ *
+ * Weight tile image: on the fused path (S % 4 == 0, S <= 256, H <= 512) the row kernel streams
+ * the weights from a tiled copy kept in the workspace.  hwy_ppo_optimizer rewrites it with every
+ * Adam step; call hwy_ppo_sync_params once before the first hwy_ppo_forward_backward on a
+ * workspace, and again whenever params were written by anything other than hwy_ppo_optimizer
+ * (a checkpoint load, a torch optimizer step, a broadcast).
  */
 #ifndef HWY_PPO_H_
 #define HWY_PPO_H_
@@ -65,6 +71,8 @@ typedef struct hwy_ppo_args {
 int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream);
 /* clip_grad_norm_(max_grad_norm) + Adam step on params (call after any gradient all-reduce). */
 int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream);
+/* Rebuild the workspace's weight tile image from params (uses dims, params, workspace). */
+int hwy_ppo_sync_params(const hwy_ppo_args* a, void* stream);
 
 /* ActorCritic.act on a batch (replaces ppo/agent.py:86-95's forward + Normal sample + tanh +
  * squashed log-prob on the batched rollout path): dims.B rows of states [B][S] (contiguous);

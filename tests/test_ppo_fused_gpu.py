@@ -61,6 +61,7 @@ def test_fused_gradient_matches_autograd(S, H, mb):
     F = FusedPPO(b, mb, 2, use_graphs=False)
     args = F._args(s, z, lp, adv, ret, idx.data_ptr())
     F.counters.zero_()
+    F.sync_params(args)
     F._fwd_bwd(args)
     torch.cuda.synchronize()
     ga = dict(a.actor_critic.named_parameters())
@@ -120,6 +121,17 @@ def test_fused_optimizer_matches_torch_adam_on_identical_grads():
         torch.cuda.synchronize()
         for name in pa:
             torch.testing.assert_close(pb[name], pa[name], rtol=1e-5, atol=1e-7, msg=name)
+    # the weight tile image the row kernel reads was rewritten by every Adam step: a step from it
+    # equals a step from a freshly rebuilt image, bit for bit
+    s, z, lp, adv, ret, perm = _data(256, S, a)
+    idx = perm[:128].contiguous()
+    fa = F._args(s, z, lp, adv, ret, idx.data_ptr())
+    F._fwd_bwd(fa)
+    g_adam = F.grads.clone()
+    F.sync_params(fa)
+    F._fwd_bwd(fa)
+    torch.cuda.synchronize()
+    assert torch.equal(F.grads, g_adam)
 
 
 def test_fused_state_roundtrip_to_torch_optimizer(tmp_path):

@@ -8,7 +8,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import torch
 import hwy.native as native
 
-native.LIB_PATH = os.path.join(os.path.dirname(native.LIB_PATH), "libhwy_prof.so")
+native.LIB_PATH = os.environ.get("HWY_PROF_LIB") or os.path.join(os.path.dirname(native.LIB_PATH), "libhwy_prof.so")
 from hwy.ppo_native import FusedPPO
 from ppo.agent import PPOAgent
 

@@ -1,0 +1,35 @@
+"""Times the fused PPO update (graph of ppo_rows / ppo_wgrad / ppo_wsum / ppo_adam) at the bench
+minibatch (development aid): probe_ppo_time.py [H] [reps]; HWY_LIB overrides the library."""
+import os, sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "highway-rope-ppo_amd"))
+import torch
+import hwy.native as native
+
+if os.environ.get("HWY_LIB"):
+    native.LIB_PATH = os.environ["HWY_LIB"]
+from hwy.ppo_native import FusedPPO
+from ppo.agent import PPOAgent
+
+dev = torch.device("cuda", 0)
+S, H, mb, nmb = 60, int(sys.argv[1]) if len(sys.argv) > 1 else 256, 4096, 32
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+torch.manual_seed(0)
+ag = PPOAgent(S, 2, lr=3e-4, epochs=1, hidden_dim=H, device=dev, use_graphs=False, backend="hip")
+n = mb * nmb
+s = torch.randn(n, S, device=dev)
+z = torch.randn(n, 2, device=dev)
+lp = torch.randn(n, device=dev) - 2
+adv = torch.randn(n, device=dev)
+ret = torch.randn(n, device=dev)
+perm = torch.randperm(n, device=dev)
+F = FusedPPO(ag, mb, nmb, use_graphs=True)
+F.run(s, z, lp, adv, ret, perm)
+torch.cuda.synchronize()
+ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+ev0.record()
+for _ in range(reps):
+    F.run(s, z, lp, adv, ret, perm)
+ev1.record()
+torch.cuda.synchronize()
+print(f"H={H}: {ev0.elapsed_time(ev1) / (reps * nmb) * 1e3:.1f} us per minibatch step", flush=True)
