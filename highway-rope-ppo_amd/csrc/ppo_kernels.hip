@@ -497,10 +497,22 @@ struct HeadArgs {
 
 constexpr int kHeadMaxQ = 8;  // H <= 512
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+// v + DPP-moved copy of v (lanes outside row_mask add 0)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_add(float v) {
+  const int m = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROWS, 0xf, false);
+  return v + __builtin_bit_cast(float, m);
+}
+// wave sum with DPP steps (pairs, quads, 8, 16 lanes, then rows by broadcast), total read from
+// lane 63 as a wave-uniform value
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v = dpp_add<0xB1, 0xf>(v);   // quad_perm(1,0,3,2)
+  v = dpp_add<0x4E, 0xf>(v);   // quad_perm(2,3,0,1)
+  v = dpp_add<0x141, 0xf>(v);  // row_half_mirror
+  v = dpp_add<0x140, 0xf>(v);  // row_mirror
+  v = dpp_add<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+  v = dpp_add<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 
 __global__ void __launch_bounds__(256) ppo_head(HeadArgs h) {
@@ -550,7 +562,8 @@ __global__ void __launch_bounds__(256) ppo_head(HeadArgs h) {
     const long src = (long)h.idx[b];
     const float z0 = h.pre_tanh[src * 2], z1 = h.pre_tanh[src * 2 + 1];
     const float old = h.old_logp[src], ad = h.adv[src], rt = h.ret[src];
-    const float mu0 = wave_sum(p0) + ba0, mu1 = wave_sum(p1) + ba1, val = wave_sum(pv) + bcv;
+    const float mu0 = wave_sum_dpp(p0) + ba0, mu1 = wave_sum_dpp(p1) + ba1,
+                val = wave_sum_dpp(pv) + bcv;
     const float d0 = z0 - mu0, d1 = z1 - mu1;
     const float t0 = tanhf(z0), t1 = tanhf(z1);
     const float lp0 = -(d0 * d0) / (2.0f * var0) - lsc0 - LOG_SQRT_2PI;
@@ -890,6 +903,30 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   WRing<TW, D, 7, true> R;
   ring_setup(R, P, r.off, S, H, w * (H / NW), r.tiles);
   R.prime();
+  // the loss head's inputs and weights, loaded now so that their latency hides behind the
+  // forward (wave w takes rows RPW*w ..; the row values are wave-uniform)
+  float hz0[RPW], hz1[RPW], hold[RPW], hadv[RPW], hret[RPW];
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int lr = min(RPW * wu + rr, nrows - 1);
+    const long src = (long)r.idx[row0 + lr];
+    hz0[rr] = r.pre_tanh[src * 2];
+    hz1[rr] = r.pre_tanh[src * 2 + 1];
+    hold[rr] = r.old_logp[src];
+    hadv[rr] = r.adv[src];
+    hret[rr] = r.ret[src];
+  }
+  float wa0[QH], wa1[QH], wc[QH];
+#pragma unroll
+  for (int q = 0; q < QH; ++q) {
+    const int col = lane + 64 * q;
+    wa0[q] = P[r.off[P_WA2] + col];
+    wa1[q] = P[r.off[P_WA2] + H + col];
+    wc[q] = P[r.off[P_WC2] + col];
+  }
+  const float ba0 = P[r.off[P_BA2]], ba1 = P[r.off[P_BA2] + 1], bcv = P[r.off[P_BC2]];
+  const float ls0 = P[r.off[P_LOGSTD]], ls1 = P[r.off[P_LOGSTD] + 1];
   rows_forward<QH, NW>(R, r.states, r.idx, S, nrows, row0, P, r.off, X, H1, H2, AC, r.xg, r.h1,
                        r.h2 PSEC_ARGS);
   PSEC(3);
@@ -903,17 +940,8 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   float s_dba0 = 0, s_dba1 = 0, s_dbc = 0, s_dls0 = 0, s_dls1 = 0;
   float s_pg = 0, s_vf = 0, s_clip = 0, s_kl = 0;
   {
-    float wa0[QH], wa1[QH], wc[QH];
 #pragma unroll
-    for (int q = 0; q < QH; ++q) {
-      const int col = lane + 64 * q;
-      wa0[q] = P[r.off[P_WA2] + col];
-      wa1[q] = P[r.off[P_WA2] + H + col];
-      wc[q] = P[r.off[P_WC2] + col];
-      ga0[q] = ga1[q] = gc[q] = 0.0f;
-    }
-    const float ba0 = P[r.off[P_BA2]], ba1 = P[r.off[P_BA2] + 1], bcv = P[r.off[P_BC2]];
-    const float ls0 = P[r.off[P_LOGSTD]], ls1 = P[r.off[P_LOGSTD] + 1];
+    for (int q = 0; q < QH; ++q) ga0[q] = ga1[q] = gc[q] = 0.0f;
     // torch Normal: scale = exp(log_std); var = scale**2; log_scale = log(scale)
     const float sc0 = expf(ls0), sc1 = expf(ls1);
     const float var0 = sc0 * sc0, var1 = sc1 * sc1;
@@ -921,26 +949,37 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
     const float LOG_SQRT_2PI = 0.91893853320467274178f;
     const float invB = 1.0f / (float)r.B;
     const float lo = 1.0f - r.eps_clip, hi = 1.0f + r.eps_clip;
+    // the heads' dot products of all this wave's rows first, so that their reductions overlap
+    float hmu0[RPW], hmu1[RPW], hval[RPW];
+#pragma unroll
     for (int rr = 0; rr < RPW; ++rr) {
-      const int lr = RPW * w + rr;
-      if (lr >= nrows) break;
-      const int b = row0 + lr;
-      float* arow = AC + lr * PA;
-      float a[QH], cc[QH];
+      const float* arow = AC + min(RPW * w + rr, nrows - 1) * PA;
       float p0 = 0.0f, p1 = 0.0f, pv = 0.0f;
 #pragma unroll
       for (int q = 0; q < QH; ++q) {
         const int col = lane + 64 * q;
-        a[q] = arow[col];
-        cc[q] = arow[H + col];
-        p0 += a[q] * wa0[q];
-        p1 += a[q] * wa1[q];
-        pv += cc[q] * wc[q];
+        const float av = arow[col], cv = arow[H + col];
+        p0 += av * wa0[q];
+        p1 += av * wa1[q];
+        pv += cv * wc[q];
       }
-      const long src = (long)r.idx[b];
-      const float z0 = r.pre_tanh[src * 2], z1 = r.pre_tanh[src * 2 + 1];
-      const float old = r.old_logp[src], ad = r.adv[src], rt = r.ret[src];
-      const float mu0 = wave_sum(p0) + ba0, mu1 = wave_sum(p1) + ba1, val = wave_sum(pv) + bcv;
+      hmu0[rr] = wave_sum_dpp(p0) + ba0;
+      hmu1[rr] = wave_sum_dpp(p1) + ba1;
+      hval[rr] = wave_sum_dpp(pv) + bcv;
+    }
+    PSEC(7);
+    // the per-row scalar part once for all this wave's rows: row rr on lane rr
+    float c_dmu0, c_dmu1, c_dv, c_dls0, c_dls1, c_pg, c_vf, c_clip, c_kl;
+    {
+      const int rs = min(lane, RPW - 1);
+      float z0 = hz0[0], z1 = hz1[0], old = hold[0], ad = hadv[0], rt = hret[0];
+      float mu0 = hmu0[0], mu1 = hmu1[0], val = hval[0];
+#pragma unroll
+      for (int rr = 1; rr < RPW; ++rr)
+        if (rs == rr) {
+          z0 = hz0[rr], z1 = hz1[rr], old = hold[rr], ad = hadv[rr], rt = hret[rr];
+          mu0 = hmu0[rr], mu1 = hmu1[rr], val = hval[rr];
+        }
       const float d0 = z0 - mu0, d1 = z1 - mu1;
       const float t0 = tanhf(z0), t1 = tanhf(z1);
       const float lp0 = -(d0 * d0) / (2.0f * var0) - lsc0 - LOG_SQRT_2PI;
@@ -955,32 +994,52 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
       // torch.min / clamp backward: ties split the gradient evenly
       const float wsel = s1 < s2 ? 1.0f : (s1 > s2 ? inr : 0.5f * (1.0f + inr));
       const float dlogp = -invB * ad * wsel * ratio;  // d(actor_loss)/d(logp)
-      const float dmu0 = dlogp * d0 / var0, dmu1 = dlogp * d1 / var1;
-      const float dv = r.value_coef * 2.0f * (val - rt) * invB;
+      c_dmu0 = dlogp * d0 / var0;
+      c_dmu1 = dlogp * d1 / var1;
+      c_dv = r.value_coef * 2.0f * (val - rt) * invB;
+      c_dls0 = dlogp * ((d0 * d0) / var0 - 1.0f);
+      c_dls1 = dlogp * ((d1 * d1) / var1 - 1.0f);
+      c_pg = -fminf(s1, s2);
+      c_vf = (val - rt) * (val - rt);
+      c_clip = fabsf(ratio - 1.0f) > r.eps_clip ? 1.0f : 0.0f;
+      c_kl = (ratio - 1.0f) - log_ratio;
+    }
+    auto lane_f = [](float v, int l) {
+      return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+    };
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr) {
+      const int lr = RPW * w + rr;
+      if (lr >= nrows) break;
+      const int b = row0 + lr;
+      float* arow = AC + lr * PA;
+      const float dmu0 = lane_f(c_dmu0, rr), dmu1 = lane_f(c_dmu1, rr), dv = lane_f(c_dv, rr);
       float* grow = r.dac + (long)b * 2 * H;
 #pragma unroll
       for (int q = 0; q < QH; ++q) {
         const int col = lane + 64 * q;
-        const float da = a[q] > 0.0f ? (dmu0 * wa0[q] + dmu1 * wa1[q]) : 0.0f;
-        const float dc = cc[q] > 0.0f ? dv * wc[q] : 0.0f;
+        const float a = arow[col], cc = arow[H + col];
+        const float da = a > 0.0f ? (dmu0 * wa0[q] + dmu1 * wa1[q]) : 0.0f;
+        const float dc = cc > 0.0f ? dv * wc[q] : 0.0f;
         arow[col] = da;
         arow[H + col] = dc;
         grow[col] = da;
         grow[H + col] = dc;
-        ga0[q] += dmu0 * a[q];
-        ga1[q] += dmu1 * a[q];
-        gc[q] += dv * cc[q];
+        ga0[q] += dmu0 * a;
+        ga1[q] += dmu1 * a;
+        gc[q] += dv * cc;
       }
       s_dba0 += dmu0;
       s_dba1 += dmu1;
       s_dbc += dv;
-      s_dls0 += dlogp * ((d0 * d0) / var0 - 1.0f);
-      s_dls1 += dlogp * ((d1 * d1) / var1 - 1.0f);
-      s_pg += -fminf(s1, s2);
-      s_vf += (val - rt) * (val - rt);
-      s_clip += fabsf(ratio - 1.0f) > r.eps_clip ? 1.0f : 0.0f;
-      s_kl += (ratio - 1.0f) - log_ratio;
+      s_dls0 += lane_f(c_dls0, rr);
+      s_dls1 += lane_f(c_dls1, rr);
+      s_pg += lane_f(c_pg, rr);
+      s_vf += lane_f(c_vf, rr);
+      s_clip += lane_f(c_clip, rr);
+      s_kl += lane_f(c_kl, rr);
     }
+    PSEC(11);
     if (blockIdx.x == 0 && t == 0) {
       r.counters[0] += 1;  // Adam step t for this minibatch
       r.counters[1] += 1;  // metrics row (this step writes row counters[1]-1)
@@ -1092,7 +1151,8 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_act(ActArgs r) {
       p1 += a * wa1[q];
       pv += c * wc[q];
     }
-    const float mu0 = wave_sum(p0) + ba0, mu1 = wave_sum(p1) + ba1, val = wave_sum(pv) + bcv;
+    const float mu0 = wave_sum_dpp(p0) + ba0, mu1 = wave_sum_dpp(p1) + ba1,
+                val = wave_sum_dpp(pv) + bcv;
     if (lane == 0) {
       float z0 = mu0, z1 = mu1, lp = 0.0f;
       if (r.noise) {

@@ -41,8 +41,8 @@ L.hwy_ppo_debug_sections(buf, 1)
 steps = reps * nmb
 print(f"H={H}: {ev0.elapsed_time(ev1) / steps * 1e3:.1f} us per minibatch step (graph, incl. adam)")
 n1 = (mb + 15) // 16
-names = {0: "rows: gather", 1: "rows: h1", 2: "rows: h2", 3: "rows: ac", 4: "rows: head",
-         5: "rows: dh2", 6: "rows: dh1"}
+names = {0: "rows: gather", 1: "rows: h1", 2: "rows: h2", 3: "rows: ac", 7: "rows: head sums",
+         11: "rows: head rows", 4: "rows: head sync", 5: "rows: dh2", 6: "rows: dh1"}
 tot = sum(buf[i] for i in names)
 for i, nm in names.items():
     print(f"  {nm:22s} {buf[i] / (steps * n1):10,.0f} clk/WG  {100 * buf[i] / tot:5.1f}%")
