@@ -787,14 +787,14 @@ __device__ __forceinline__ void ring_setup(WRing<TW, D, NSEG, TL>& R, const floa
 
 // C element (t, r) of lane: row 4*(lane>>4) + r, column n_base + 16 t + (lane & 15)
 template <int QH>
-__device__ __forceinline__ void row_epi_bias_relu(const f32x4 (&acc)[QH], const float* bias,
+__device__ __forceinline__ void row_epi_bias_relu(const f32x4 (&acc)[QH], const float (&bias)[QH],
                                                   float* out, int po, float* gout, int ldg,
                                                   int nrows, int n_base) {
   const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
 #pragma unroll
   for (int t = 0; t < QH; ++t) {
     const int n = n_base + 16 * t + c;
-    const float bn = bias[n];
+    const float bn = bias[t];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = 4 * g + r;
@@ -838,6 +838,16 @@ __device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG, TL>& R
   constexpr int NT = 64 * NW;
   constexpr int PH = H + 4, PA = 2 * H + 4;
   const int t = threadIdx.x;
+  // this wave's bias values of the four layers, loaded ahead of their epilogues
+  float bias[4][TW];
+  {
+    const int c = t & 15;
+    const int64_t bo[4] = {off[P_B1], off[P_B2], off[P_BA1], off[P_BC1]};
+#pragma unroll
+    for (int l = 0; l < 4; ++l)
+#pragma unroll
+      for (int u = 0; u < TW; ++u) bias[l][u] = P[bo[l] + R.n_base + 16 * u + c];
+  }
   // zero-padded to whole ring groups of 16-deep blocks
   const int Sp = ((S + 15) / 16 + D - 1) / D * D * 16, px = row_pitch(Sp);
   // states rows, zero-padded to Sp columns and 16 rows
@@ -858,24 +868,24 @@ __device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG, TL>& R
   // h1 = relu(x W1^T + b1)
   zero_acc(acc);
   R.template run<0>(X, px, acc);
-  row_epi_bias_relu<TW>(acc, P + off[P_B1], H1, PH, h1g ? h1g + (long)row0 * H : nullptr, H,
+  row_epi_bias_relu<TW>(acc, bias[0], H1, PH, h1g ? h1g + (long)row0 * H : nullptr, H,
                         nrows, nb);
   __syncthreads();
   PSEC(1);
   // h2 = relu(h1 W2^T + b2)
   zero_acc(acc);
   R.template run<1>(H1, PH, acc);
-  row_epi_bias_relu<TW>(acc, P + off[P_B2], H2, PH, h2g ? h2g + (long)row0 * H : nullptr, H,
+  row_epi_bias_relu<TW>(acc, bias[1], H2, PH, h2g ? h2g + (long)row0 * H : nullptr, H,
                         nrows, nb);
   __syncthreads();
   PSEC(2);
   // [a1 | c1] = relu(h2 [Wa1; Wc1]^T + [ba1; bc1])
   zero_acc(acc);
   R.template run<2>(H2, PH, acc);
-  row_epi_bias_relu<TW>(acc, P + off[P_BA1], AC, PA, nullptr, 0, nrows, nb);
+  row_epi_bias_relu<TW>(acc, bias[2], AC, PA, nullptr, 0, nrows, nb);
   zero_acc(acc);
   R.template run<3>(H2, PH, acc);
-  row_epi_bias_relu<TW>(acc, P + off[P_BC1], AC + H, PA, nullptr, 0, nrows, nb);
+  row_epi_bias_relu<TW>(acc, bias[3], AC + H, PA, nullptr, 0, nrows, nb);
   __syncthreads();
 }
 
