@@ -1554,7 +1554,9 @@ __device__ __forceinline__ void write_tiles(const OptArgs& o, int64_t i, float v
   const int64_t H = o.H;
   int64_t j = i - o.o_w1;
   if (j >= 0 && j < H * o.S) {  // W1 [H][S]: forward only, B[k][n] = W1[n][k]
-    const int n = (int)(j / o.S), k = (int)(j - (int64_t)n * o.S);
+    // j / S in float: (j + 1/2) / S stays >= 1/(2S) away from an integer, far above rounding
+    const int n = (int)(((float)j + 0.5f) * (1.0f / (float)o.S));
+    const int k = (int)(j - (int64_t)n * o.S);
     o.tiles[T.f1 + tile_index(k, n, o.sb)] = v;
     return;
   }
@@ -1564,7 +1566,8 @@ __device__ __forceinline__ void write_tiles(const OptArgs& o, int64_t i, float v
   for (int q = 0; q < 3; ++q) {
     j = i - offs[q];
     if (j >= 0 && j < H * H) {  // [H][H]: forward B = W^T, backward B = W
-      const int n = (int)(j / H), k = (int)(j - (int64_t)n * H);
+      const int n = (int)(((float)j + 0.5f) * (1.0f / (float)o.H));
+      const int k = (int)(j - (int64_t)n * H);
       o.tiles[fwd[q] + tile_index(k, n, o.hb)] = v;
       o.tiles[bwd[q] + tile_index(n, k, o.hb)] = v;
       return;
@@ -1627,7 +1630,12 @@ __global__ void __launch_bounds__(kRedThreads) ppo_sumsq(const float* g, int64_t
 
 __global__ void __launch_bounds__(256) ppo_adam(OptArgs o) {
   __shared__ float red[4];
-  __shared__ float coef_s;
+  __shared__ float coef_s, step_s, bc2s_s;
+  // this thread's element first: its loads overlap the norm reduction's
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool live = i < o.numel;
+  const int64_t ii = live ? i : 0;
+  const float g_raw = o.grads[ii], m_old = o.m[ii], v_old = o.v[ii], p_old = o.params[ii];
   float s = 0.0f;
   for (int k = threadIdx.x; k < o.nred; k += 256) s += o.norm_part[k];
 #pragma unroll
@@ -1638,25 +1646,31 @@ __global__ void __launch_bounds__(256) ppo_adam(OptArgs o) {
     const float total = sqrtf(((red[0] + red[1]) + red[2]) + red[3]);
     const float c = o.max_norm / (total + 1e-6f);
     coef_s = c < 1.0f ? c : 1.0f;
+    // torch.optim.Adam (foreach, non-capturable): bias corrections in double on the host side
+    // (beta ** t by binary powering: a few dependent multiplies instead of a double pow())
+    const int t = o.counters[0];
+    double p1 = 1.0, p2 = 1.0, b1 = (double)o.beta1, b2 = (double)o.beta2;
+    for (int e = t; e > 0; e >>= 1) {
+      if (e & 1) p1 *= b1, p2 *= b2;
+      b1 *= b1, b2 *= b2;
+    }
+    const double bc1 = 1.0 - p1;
+    const double bc2 = 1.0 - p2;
+    step_s = (float)((double)o.lr / bc1);
+    bc2s_s = (float)sqrt(bc2);
   }
   __syncthreads();
   const float coef = coef_s;
-  const int t = o.counters[0];
-  // torch.optim.Adam (foreach, non-capturable): bias corrections in double on the host side
-  const double bc1 = 1.0 - pow((double)o.beta1, (double)t);
-  const double bc2 = 1.0 - pow((double)o.beta2, (double)t);
-  const float step_size = (float)((double)o.lr / bc1);
-  const float bc2_sqrt = (float)sqrt(bc2);
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= o.numel) return;
-  const float g = o.grads[i] * coef;
-  float mm = o.m[i], vv = o.v[i];
+  const float step_size = step_s, bc2_sqrt = bc2s_s;
+  if (!live) return;
+  const float g = g_raw * coef;
+  float mm = m_old, vv = v_old;
   mm = mm + (1.0f - o.beta1) * (g - mm);  // exp_avg.lerp_(grad, 1 - beta1)
   vv = vv * o.beta2 + (1.0f - o.beta2) * g * g;
   o.m[i] = mm;
   o.v[i] = vv;
   const float denom = sqrtf(vv) / bc2_sqrt + o.eps;
-  const float pn = o.params[i] - step_size * (mm / denom);
+  const float pn = p_old - step_size * (mm / denom);
   o.params[i] = pn;
   if (o.tiles) write_tiles(o, i, pn);
 }
