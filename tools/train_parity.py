@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Reward-parity training runs: the reference's north-star cell on the MI355X env.
+
+Runs `ExperimentRunner.launch` (experiments/runner.py, the reference's runner sequence,
+/root/reference/experiments/runner.py:73-122) for the reference experiment
+`sorted_lr0.0003_hidden_dim256_clip_eps0.2_entropy_coef0.005_epochs8_batch_size64` at the given
+seeds, 1500 episodes, eval every 50 episodes, and compares `final_reward` (mean of the last 10
+evals, each the mean of 5 deterministic episodes seeded exp_seed+1000+k;
+training/routine.py:181-186,292) with the reference's published value for the same seed
+(artifacts/combined_validated_data-final-run.csv rows sorted_..._hidden_dim256_..._batch_size64:
+seed 42 136.8270, 1042 127.8022, 2042 132.6172; mean 132.42).
+
+Usage (GPU box):  python tools/train_parity.py --seeds 42 --out gpurun_out/train
+    --num-envs 1   the reference's own loop (1 env, batch-1 select_action, 2048-step updates)
+    --num-envs E   the lockstep loop (E envs, same hyperparameters, same episode budget)
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "highway-rope-ppo_amd"))
+
+REFERENCE_FINAL = {42: 136.8270, 1042: 127.8022, 2042: 132.6172}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--seeds", type=int, nargs="+", default=[42])
+    p.add_argument("--episodes", type=int, default=1500)
+    p.add_argument("--num-envs", type=int, default=1)
+    p.add_argument("--out", default="gpurun_out/train")
+    args = p.parse_args()
+
+    out = os.path.abspath(args.out)
+    os.makedirs(out, exist_ok=True)
+    import torch
+
+    from config.base_config import HIGHWAY_CONFIG
+    from experiments.config import Condition, ConditionHP, Experiment
+    from experiments.runner import ExperimentRunner
+
+    results = []
+    for seed in args.seeds:
+        name = ("sorted_lr0.0003_hidden_dim256_clip_eps0.2_entropy_coef0.005_epochs8_"
+                f"batch_size64_seed{seed}" + (f"_envs{args.num_envs}" if args.num_envs > 1 else ""))
+        hp = ConditionHP(lr=3e-4, clip_eps=0.2, epochs=8, batch_size=64, hidden_dim=256)
+        hp.entropy_coef = 0.005
+        extra = {"log_interval": 50, "eval_interval": 50}
+        if args.num_envs > 1:
+            extra["num_envs"] = args.num_envs
+        exp = Experiment(name=name, condition=Condition.SORTED, hp=hp, seed=seed,
+                         max_episodes=args.episodes, target_reward=130.0, extra=extra)
+        run_dir = os.path.join(out, f"seed{seed}")
+        os.makedirs(run_dir, exist_ok=True)
+        cwd = os.getcwd()
+        os.chdir(run_dir)
+        t0 = time.time()
+        try:
+            res = ExperimentRunner(HIGHWAY_CONFIG).launch(exp)
+        finally:
+            os.chdir(cwd)
+        wall = time.time() - t0
+        row = {"seed": seed, "experiment": name, "status": res["status"], "wall_s": round(wall, 1),
+               "num_envs": args.num_envs, "episodes": args.episodes,
+               "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else "cpu"}
+        if res["status"] == "COMPLETED":
+            avg = res["avg_rewards"]
+            hist = res["metrics_history"]
+            row.update(final_reward=round(float(avg[-1]), 4), max_reward=round(float(max(avg)), 4),
+                       evals=[round(float(x), 2) for x in hist.get("eval_rewards", [])])
+            ref = REFERENCE_FINAL.get(seed)
+            if ref is not None:
+                row.update(reference_final_reward=ref,
+                           delta=round(float(avg[-1]) - ref, 4))
+        else:
+            row["error"] = res.get("error_message")
+        results.append(row)
+        print(json.dumps(row), flush=True)
+        with open(os.path.join(out, "summary.jsonl"), "a") as f:
+            f.write(json.dumps(row) + "\n")
+    done = [r for r in results if "final_reward" in r]
+    if done:
+        mean = sum(r["final_reward"] for r in done) / len(done)
+        print(json.dumps({"mean_final_reward": round(mean, 4), "reference_mean": 132.42,
+                          "n": len(done)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
