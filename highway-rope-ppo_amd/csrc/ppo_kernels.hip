@@ -18,6 +18,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "hwy_ppo.h"
 
@@ -64,6 +65,9 @@ constexpr int kKStep = 32;
 constexpr int kHeadRows = 16;  // minibatch rows per head workgroup (4 per wave)
 constexpr int kRowTile = 16;   // minibatch rows per ppo_rows workgroup
 constexpr int kMaxRowS = 256;  // states dim bound of the fused path (LDS)
+constexpr int kWgTM = 128, kWgTN = 64;          // ppo_wgrad output tile
+constexpr int kWgWaves = 8;                     // ppo_wgrad waves (2 per SIMD)
+constexpr int kWgPart = kWgTM * kWgTN + kWgTM;  // floats per partial tile (+ bias sums)
 
 struct GemmArgs {
   int M, N, K;
@@ -397,7 +401,7 @@ struct Work {
   float *slab_2, *bias_2;    // [s2][H][H], [s2][H]
   float *slab_1, *bias_1;    // [s1][H][S], [s1][H]
   float *norm_part;          // [max(nred, nred2)]
-  float *wg_slab;            // fused: [ntile][split][64*64 + 64] partial tiles
+  float *wg_slab;            // fused: [ntile][split][kWgPart] partial tiles
   float *xg;                 // fused: [B][S] gathered states
   float *wtile;              // fused: weight tile image (TileGeom)
   int nhead, HP, sa, s2, s1, ca, c2, c1, nred;
@@ -436,20 +440,22 @@ inline Work carve(const hwy_ppo_dims& d, void* ws, int64_t* bytes_out) {
   w.nred = (int)((L.numel + kRedThreads - 1) / kRedThreads);
   w.fused = fused_ok(d);
   w.n1 = (B + kRowTile - 1) / kRowTile;
-  w.tac = (2 * H / 64) * (H / 64);
-  w.t2 = (H / 64) * (H / 64);
-  w.t1 = (H / 64) * ((S + 63) / 64);
+  const int tmh = (H + kWgTM - 1) / kWgTM, tnh = (H + kWgTN - 1) / kWgTN;
+  w.tac = ((2 * H + kWgTM - 1) / kWgTM) * tnh;
+  w.t2 = tmh * tnh;
+  w.t1 = tmh * ((S + kWgTN - 1) / kWgTN);
   w.nh = (3 * H + 9 + 63) / 64;
   const int ntile = w.tac + w.t2 + w.t1;
-  // enough row splits to put ~256 workgroups on the chip, at least one 64-row chunk each
-  w.split = std::max(1, std::min({8, 512 / ntile, (B + 63) / 64}));  // ~2 workgroups per CU
+  // row slices per tile: one workgroup per CU (~256 on the chip), at least one 64-row chunk
+  // each, at most 8 (one per XCD)
+  w.split = std::max(1, std::min({8, 256 / ntile, (B + 63) / 64}));
   w.grid2 = ntile * w.split + w.nh;
-  w.nred2 = w.nh + 4 * ntile;
+  w.nred2 = w.nh + ntile * (kWgTM * kWgTN / 1024);
   const int64_t head_rows = w.fused ? std::max<int64_t>(w.nhead, w.n1) : w.nhead;
   const int64_t norm_n = w.fused ? std::max(w.nred, w.nred2) : w.nred;
   // the fused path needs no split-K slabs of full weight size, only the per-split tiles
   const int64_t sa = w.fused ? 0 : w.sa, s2 = w.fused ? 0 : w.s2, s1 = w.fused ? 0 : w.s1;
-  const int64_t wg_slab_n = w.fused ? (int64_t)ntile * w.split * (64 * 64 + 64) : 0;
+  const int64_t wg_slab_n = w.fused ? (int64_t)ntile * w.split * kWgPart : 0;
   const int64_t xg_n = w.fused ? (int64_t)B * S : 0;
   rows_blocks(S, H, &w.sb, &w.hb);
   const int64_t tile_n = w.fused ? tile_geom(S, H, w.sb, w.hb).total : 0;
@@ -1185,11 +1191,31 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_act(ActArgs r) {
 }
 
 // ----------------------------------------------------------------------------- weight grads
-// ppo_wgrad: every weight gradient as a full-K (= minibatch) 32x32 tile -- no split-K slabs --
-// plus the bias column sums, the head-parameter sums over the ppo_rows partials, the metrics
-// row and one sum-of-squares partial per workgroup for clip_grad_norm_.  Tiles: dWac = dac^T h2
-// (rows < H -> Wa1, >= H -> Wc1), dW2 = dh2^T h1, dW1 = dh1^T gather(states); 4 waves split the
-// minibatch rows and their tiles are summed in a fixed order (deterministic).
+// ppo_wgrad: every weight gradient of the minibatch step (the autograd of ppo/agent.py:241-248
+// for the four hidden layers), the bias column sums, the head-parameter sums over the ppo_rows
+// partials, the metrics row and the sum-of-squares partials of clip_grad_norm_ (:249-251).
+//
+// Output tiles are 128 x 64 (dWac = dac^T h2: rows < H -> Wa1, >= H -> Wc1; dW2 = dh2^T h1;
+// dW1 = dh1^T gather(states)).  Workgroup id = tile * split + z: slice z of the minibatch rows
+// (B / split rows, split = 8 at the bench shapes) goes to workgroup id % 8 = the XCD the
+// dispatcher places it on, so each XCD reads one 1/8 row slice (~3 MB at B = 4096, H = 256) and
+// keeps it in its own L2 across all the tiles.  One workgroup per CU (96 KB LDS), 4 waves; each
+// wave accumulates a 64 x 32 block as two 32x32 v_mfma_f32_32x32x2_f32 accumulators that share
+// the B operand.
+//
+// K (the minibatch rows) runs in 64-row chunks staged through LDS as [feature][row] images: each
+// thread loads 4 rows x 4 features (four float4 row segments, coalesced), transposes them in
+// registers and stores 4 float4 row-quads.  In the MFMA loop lane (l32, h) reads the float4 of
+// rows 8G + 4h .. 8G + 4h + 3 of its feature, one ds_read_b128 per 4 MFMA steps; k-step j of
+// group G then sums rows 8G + j and 8G + 4 + j (a permutation of the chunk, which the sum does
+// not see).  Quad q of feature row m is stored at slot q ^ wg_swz(m): conflict-free for both the
+// transposing ds_write_b128 (8-lane groups, m = 4c + i) and the ds_read_b128 (16-lane groups).
+//
+// The next chunk's global loads are issued before a chunk's MFMAs and its transposing LDS stores
+// are interleaved into them (two selects per MFMA), so one wave per SIMD keeps the matrix pipe
+// busy.  The split partial tiles go to a slab that ppo_wsum sums in split order (the kernel
+// boundary is the one L2 writeback that makes the other XCDs' partials visible; a last-arriver
+// reduction inside this kernel paid an agent-scope L2 writeback per workgroup, ~20 us).
 struct WgArgs {
   int B, S, H;
   const float *dac, *h2, *dh2, *h1, *dh1, *xg;
@@ -1197,16 +1223,17 @@ struct WgArgs {
   int64_t off[13];
   const float* head_part;
   int nhp, HP;
-  float* norm_part;
-  int tac, t2, t1, nh;  // 64x64 tiles per region, head-sum workgroups
-  int split;            // minibatch-row splits per tile (workgroups per tile)
-  float* slab;          // [tiles][split][64*64 + 64] partial tiles + bias partials
+  float* norm_part;     // [nh] head-sum partials, then [ntile] tile partials
+  int tac, t2, t1, nh;  // 128x64 tiles per region, head-sum workgroups
+  int split;            // minibatch-row slices per tile (workgroups per tile)
+  float* slab;          // [tiles][split][128*64 + 128] partial tiles + bias partials
   float entropy_coef, value_coef, ent_const;
   const float* params;
   float* metrics;
   int32_t* counters;
 };
 
+template <int NW = 4>
 __device__ __forceinline__ float block_sum4(float v, float* red) {
   const int t = threadIdx.x;
 #pragma unroll
@@ -1214,239 +1241,331 @@ __device__ __forceinline__ float block_sum4(float v, float* red) {
   __syncthreads();
   if ((t & 63) == 0) red[t >> 6] = v;
   __syncthreads();
-  return ((red[0] + red[1]) + red[2]) + red[3];
+  float s = red[0];
+#pragma unroll
+  for (int i = 1; i < NW; ++i) s += red[i];
+  return s;
 }
 
-// LDS image of a 64-row chunk: row k, column col at k*64 + (col ^ 32*(k&1)), so the two lane
-// halves of an MFMA operand read (rows 2s, 2s+1) hit disjoint banks
-__device__ __forceinline__ int wg_sw(int k, int col) { return k * 64 + (col ^ ((k & 1) << 5)); }
+// slot swizzle of an LDS image with 64-float feature rows (16 row-quads): bijective in m >> 2
+// mod 8 for each m & 3 (the store groups) and in m mod 16 over every ds_read_b128 lane group
+__device__ __forceinline__ int wg_swz(int m) {
+  return (((m >> 2) ^ ((m & 3) >> 1)) & 7) | ((m & 1) << 3);
+}
+__device__ __forceinline__ int wg_at(int m, int q) { return m * 64 + 4 * (q ^ wg_swz(m)); }
 
-__global__ void __launch_bounds__(256) ppo_wgrad(WgArgs a) {
+// head parameters (the ppo_rows partials summed in row-block order) + the metrics row
+__device__ void wgrad_head(const WgArgs& a, int hid, float* lds, float* red) {
+  float(*tile)[64] = reinterpret_cast<float(*)[64]>(lds);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, H = a.H;
+  const int e = hid * 64 + lane;
+  const int ne = 3 * H + 9;
+  const int per = (a.nhp + kWgWaves - 1) / kWgWaves, p0 = w * per, p1 = min(a.nhp, p0 + per);
+  float s = 0.0f, sq = 0.0f;
+  if (e < ne) {
+    for (int pb = p0; pb < p1; pb += 16) {  // 16 loads in flight, summed in row order
+      float pv[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        pv[u] = pb + u < p1 ? a.head_part[(long)(pb + u) * a.HP + e] : 0.0f;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += pv[u];
+    }
+  }
+  tile[w][lane] = s;
+  __syncthreads();
+  if (t < 64 && e < ne) {
+    float g = tile[0][t];
+#pragma unroll
+    for (int i = 1; i < kWgWaves; ++i) g += tile[i][t];
+    long dst = -1;
+    float gv = g;
+    if (e < 2 * H) {
+      dst = a.off[P_WA2] + e;
+    } else if (e < 3 * H) {
+      dst = a.off[P_WC2] + (e - 2 * H);
+    } else {
+      const int k = e - 3 * H;
+      if (k < 2) dst = a.off[P_BA2] + k;
+      else if (k == 2) dst = a.off[P_BC2];
+      else if (k < 5) dst = a.off[P_LOGSTD] + (k - 3), gv = g - a.entropy_coef;
+    }
+    if (dst >= 0) {
+      a.grads[dst] = gv;
+      sq = gv * gv;
+    }
+    tile[0][t] = g;  // keep the totals for the metrics row
+  }
+  const float tot = block_sum4<kWgWaves>(sq, red);
+  if (t == 0) a.norm_part[hid] = tot;
+  if (3 * H >= e - lane && 3 * H < e - lane + 64 && t == 0) {
+    // metrics row (ppo/agent.py:255-262): policy, value, entropy, loss, clip count, kl
+    const int k0 = 3 * H - (e - lane);
+    const float pg = tile[0][k0 + 5], vf = tile[0][k0 + 6], clip = tile[0][k0 + 7],
+                kl = tile[0][k0 + 8];
+    const float invB = 1.0f / (float)a.B;
+    const float ls0 = a.params[a.off[P_LOGSTD]], ls1 = a.params[a.off[P_LOGSTD] + 1];
+    const float ent = (a.ent_const + logf(expf(ls0))) + (a.ent_const + logf(expf(ls1)));
+    float* m = a.metrics + (int64_t)(a.counters[1] - 1) * 6;
+    m[0] = pg * invB;
+    m[1] = vf * invB;
+    m[2] = ent;
+    m[3] = (pg * invB + a.value_coef * (vf * invB)) - a.entropy_coef * ent;
+    m[4] = clip;
+    m[5] = kl * invB;
+  }
+}
+
+__global__ void __launch_bounds__(512) ppo_wgrad(WgArgs a) {
   PSEC_DECL
-  __shared__ __attribute__((aligned(16))) float wg_lds[4 * 64 * 64];
-  __shared__ float red[4];
+  __shared__ __attribute__((aligned(16))) float wg_lds[2 * (kWgTM + kWgTN) * 64];
+  __shared__ float red[kWgWaves];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, l32 = lane & 31;
   const int H = a.H;
   const int ntile = a.tac + a.t2 + a.t1;
   int id = blockIdx.x;
-  float sq = 0.0f;
   if (id >= ntile * a.split) {  // ---- head parameters + metrics
-    float(*tile)[64] = reinterpret_cast<float(*)[64]>(wg_lds);
-    const int hid = id - ntile * a.split;
-    const int e = hid * 64 + lane;
-    const int ne = 3 * H + 9;
-    const int per = (a.nhp + 3) / 4, p0 = w * per, p1 = min(a.nhp, p0 + per);
-    float s = 0.0f;
-    if (e < ne) {
-      for (int pb = p0; pb < p1; pb += 16) {  // 16 loads in flight, summed in row order
-        float pv[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u)
-          pv[u] = pb + u < p1 ? a.head_part[(long)(pb + u) * a.HP + e] : 0.0f;
-#pragma unroll
-        for (int u = 0; u < 16; ++u) s += pv[u];
-      }
-    }
-    tile[w][lane] = s;
-    __syncthreads();
-    float g = 0.0f;
-    if (t < 64 && e < ne) {
-      g = ((tile[0][t] + tile[1][t]) + tile[2][t]) + tile[3][t];
-      long dst = -1;
-      float gv = g;
-      if (e < 2 * H) {
-        dst = a.off[P_WA2] + e;
-      } else if (e < 3 * H) {
-        dst = a.off[P_WC2] + (e - 2 * H);
-      } else {
-        const int k = e - 3 * H;
-        if (k < 2) dst = a.off[P_BA2] + k;
-        else if (k == 2) dst = a.off[P_BC2];
-        else if (k < 5) dst = a.off[P_LOGSTD] + (k - 3), gv = g - a.entropy_coef;
-      }
-      if (dst >= 0) {
-        a.grads[dst] = gv;
-        sq = gv * gv;
-      }
-      tile[0][t] = g;  // keep the totals for the metrics row
-    }
-    const float tot = block_sum4(sq, red);
-    if (t == 0) a.norm_part[hid] = tot;
-    if (3 * H >= e - lane && 3 * H < e - lane + 64 && t == 0) {
-      // metrics row (ppo/agent.py:255-262): policy, value, entropy, loss, clip count, kl
-      const int k0 = 3 * H - (e - lane);
-      const float pg = tile[0][k0 + 5], vf = tile[0][k0 + 6], clip = tile[0][k0 + 7],
-                  kl = tile[0][k0 + 8];
-      const float invB = 1.0f / (float)a.B;
-      const float ls0 = a.params[a.off[P_LOGSTD]], ls1 = a.params[a.off[P_LOGSTD] + 1];
-      const float ent = (a.ent_const + logf(expf(ls0))) + (a.ent_const + logf(expf(ls1)));
-      float* m = a.metrics + (int64_t)(a.counters[1] - 1) * 6;
-      m[0] = pg * invB;
-      m[1] = vf * invB;
-      m[2] = ent;
-      m[3] = (pg * invB + a.value_coef * (vf * invB)) - a.entropy_coef * ent;
-      m[4] = clip;
-      m[5] = kl * invB;
-    }
+    wgrad_head(a, id - ntile * a.split, wg_lds, red);
     PSEC(10);
     PSEC_FLUSH;
     return;
   }
-  // ---- a 64x64 weight-gradient tile over 1/split of the minibatch rows.  z = id % split: with
-  // split = 8 every XCD (workgroup id mod 8) works on one 1/8 slice of the minibatch rows, whose
-  // activations (~3 MB at B = 4096, H = 256) stay in that XCD's L2 for all the tiles
   const int z = id % a.split;
-  id /= a.split;
-  const int tile_id = id;
+  const int tile_id = id / a.split;
+  id = tile_id;
   const float *A, *Bm;
-  int lda, ldb, N, ntj, region;
+  int lda, ldb, M, N, ntj;
   if (id < a.tac) {  // dWac = dac^T h2
-    A = a.dac, lda = 2 * H, Bm = a.h2, ldb = H, N = H, ntj = H / 64, region = 0;
+    A = a.dac, lda = 2 * H, Bm = a.h2, ldb = H, M = 2 * H, N = H;
   } else if (id < a.tac + a.t2) {  // dW2 = dh2^T h1
     id -= a.tac;
-    A = a.dh2, lda = H, Bm = a.h1, ldb = H, N = H, ntj = H / 64, region = 1;
+    A = a.dh2, lda = H, Bm = a.h1, ldb = H, M = H, N = H;
   } else {  // dW1 = dh1^T x (gathered states rows written by ppo_rows)
     id -= a.tac + a.t2;
-    A = a.dh1, lda = H, Bm = a.xg, ldb = a.S, N = a.S, ntj = (a.S + 63) / 64, region = 2;
+    A = a.dh1, lda = H, Bm = a.xg, ldb = a.S, M = H, N = a.S;
   }
+  ntj = (N + kWgTN - 1) / kWgTN;
   const int ti = id / ntj, tj = id % ntj;
-  const int i0 = ti * 64, j0 = tj * 64;
+  const int i0 = ti * kWgTM, j0 = tj * kWgTN;
   const int rows = (a.B + a.split - 1) / a.split;
   const int kb0 = z * rows, kb1 = min(a.B, kb0 + rows);
-  // K-chunks of 64 rows: A[64][64] and B[64][64] images (pitch 64) double-buffered in LDS,
-  // the next chunk's float4s in registers while the current one feeds the MFMAs
-  float* As0 = wg_lds;
-  float* Bs0 = wg_lds + 64 * 64;
-  float* As1 = wg_lds + 2 * 64 * 64;
-  float* Bs1 = wg_lds + 3 * 64 * 64;
-  // The next two chunks' float4s stay in flight in two register sets while one chunk feeds the
-  // MFMAs from LDS (double-buffered images).  Loads are unconditional (rows past the split and
-  // columns past N are clamped into range and zeroed when stashed), so the waits are counted.
-  auto fetch = [&](int k0, f32x4(&ra)[4], f32x4(&rb)[4]) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e4 = t + 256 * q, rr = e4 >> 4, c4 = (e4 & 15) * 4;
-      const int kk = min(k0 + rr, kb1 - 1);
-      const int cb = min(j0 + c4, N - 4);
-      ra[q] = *reinterpret_cast<const f32x4*>(A + (long)kk * lda + i0 + c4);
-      rb[q] = *reinterpret_cast<const f32x4*>(Bm + (long)kk * ldb + cb);
-    }
-  };
-  auto stash = [&](float* As, float* Bs, const f32x4(&ra)[4], const f32x4(&rb)[4], int k0) {
-    const f32x4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e4 = t + 256 * q, rr = e4 >> 4, c4 = (e4 & 15) * 4;
-      const bool rok = k0 + rr < kb1;
-      *reinterpret_cast<f32x4*>(&As[wg_sw(rr, c4)]) = rok ? ra[q] : zero;
-      *reinterpret_cast<f32x4*>(&Bs[wg_sw(rr, c4)]) = (rok && j0 + c4 < N) ? rb[q] : zero;
-    }
-  };
-  const int wm = (w & 1) * 32, wn = (w >> 1) * 32;
-  f32x16 acc;
-#pragma unroll
-  for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
-  float bsum = 0.0f;  // column sums of A (bias gradient), threads 0..63, tiles with tj == 0
-  const bool do_bias = tj == 0 && t < 64;
-  auto compute = [&](const float* As, const float* Bs) {
-#pragma unroll 8
-    for (int s = 0; s < 32; ++s) {
-      const int k = 2 * s + h;
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[wg_sw(k, wm + l32)], Bs[wg_sw(k, wn + l32)],
-                                                 acc, 0, 0, 0);
-    }
-    if (do_bias) {
-#pragma unroll 8
-      for (int k = 0; k < 64; ++k) bsum += As[wg_sw(k, t)];
-    }
-  };
   const int nchunk = (kb1 - kb0 + 63) / 64;  // >= 1 (split <= B / 64)
-  f32x4 ra0[4], rb0[4], ra1[4], rb1[4];
-  fetch(kb0, ra0, rb0);
-  fetch(kb0 + 64, ra1, rb1);
-  stash(As0, Bs0, ra0, rb0, kb0);
-  fetch(kb0 + 128, ra0, rb0);
+
+  // staging (64-row chunks): A = 64 rows x 128 features, thread: features 4ca .. 4ca+3 of rows
+  // 8w + 4ra .. +3; B = 64 rows x 64 features, waves 0-3, thread: features 4cb.. of rows
+  // 16w + 4rb .. +3.  Loads are clamped into range; rows past the slice are zeroed when stored,
+  // features past M / N hold finite in-range data whose outputs are never stored.
+  const int ca = lane & 31, ra = lane >> 5, cb = lane & 15, rb = lane >> 4;
+  const bool stage_b = w < 4;
+  const float* a_src = A + min(i0 + 4 * ca, M - 4);
+  const float* b_src = Bm + min(j0 + 4 * cb, N - 4);
+  // two register sets: the loads of chunk c + 2 are in flight while chunk c computes and chunk
+  // c + 1 (loaded during chunk c - 1) is staged
+  f32x4 pa0[4], pb0[4], pa1[4], pb1[4];
+  auto fetch = [&](int k0, f32x4(&pa)[4], f32x4(&pb)[4]) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int k = min(k0 + 8 * w + 4 * ra + jj, kb1 - 1);
+      pa[jj] = *reinterpret_cast<const f32x4*>(a_src + (long)k * lda);
+    }
+    if (stage_b) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int k = min(k0 + 16 * w + 4 * rb + jj, kb1 - 1);
+        pb[jj] = *reinterpret_cast<const f32x4*>(b_src + (long)k * ldb);
+      }
+    }
+  };
+  // column sums of A for the bias (kept for every tile, used when tj == 0)
+  float bsum[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  // staging pieces: 0-1 A columns 2p, 2p+1; 2-3 B columns 2p, 2p+1 (waves 0-3).  The
+  // transposing selects write straight into the ds_write_b128 data registers.
+  auto piece = [&](float* As, float* Bs, int k0, int pc, const f32x4(&pa)[4],
+                   const f32x4(&pb)[4]) {
+    if (pc < 2) {
+      const int kr = k0 + 8 * w + 4 * ra, q = 2 * w + ra;
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        const int i = 2 * pc + ii;
+        f32x4 col;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) col[jj] = kr + jj < kb1 ? pa[jj][i] : 0.0f;
+        *reinterpret_cast<f32x4*>(&As[wg_at(4 * ca + i, q)]) = col;
+        bsum[i] += ((col[0] + col[1]) + col[2]) + col[3];
+      }
+    } else if (stage_b) {
+      const int kr = k0 + 16 * w + 4 * rb, q = 4 * w + rb;
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        const int i = 2 * (pc - 2) + ii;
+        f32x4 col;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) col[jj] = kr + jj < kb1 ? pb[jj][i] : 0.0f;
+        *reinterpret_cast<f32x4*>(&Bs[wg_at(4 * cb + i, q)]) = col;
+      }
+    }
+  };
+  // MFMA: waves w and w + 4 (the two waves of one SIMD) own the same 64 x 32 output block
+  // (two 32x32 accumulators sharing the B operand) over the even / odd 8-row groups of every
+  // chunk: four independent accumulation chains per SIMD.
+  const int kh = w >> 2, wq = w & 3;
+  const int wm = (wq & 1) * 64, wn = (wq >> 1) * 32;
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc0[q] = acc1[q] = 0.0f;
+  auto chunk = [&](const float* As, const float* Bs, float* nA, float* nB, int k_next,
+                   const f32x4(&pa)[4], const f32x4(&pb)[4], auto stash_tag) {
+    constexpr bool STASH = decltype(stash_tag)::value;
+    f32x4 x0[2], x1[2], y[2];
+    auto rd = [&](int g, int b) {  // this wave's group g = row group 2g + kh of the chunk
+      const int q = 2 * (2 * g + kh) + h;
+      x0[b] = *reinterpret_cast<const f32x4*>(&As[wg_at(wm + l32, q)]);
+      x1[b] = *reinterpret_cast<const f32x4*>(&As[wg_at(wm + 32 + l32, q)]);
+      y[b] = *reinterpret_cast<const f32x4*>(&Bs[wg_at(wn + l32, q)]);
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int b = g & 1;
+      if (g + 1 < 4) rd(g + 1, b ^ 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(x0[b][j], y[b][j], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(x1[b][j], y[b][j], acc1, 0, 0, 0);
+      }
+      if constexpr (STASH) {
+        piece(nA, nB, k_next, g, pa, pb);
+        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);  // the next group's operand reads
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU (selects, bias adds)
+          if (u == 3 || u == 6) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // ds_write
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  float* buf0 = wg_lds;
+  float* buf1 = wg_lds + (kWgTM + kWgTN) * 64;
+  // loads past the slice are clamped (harmless, never stored)
+  fetch(kb0, pa0, pb0);
+  fetch(kb0 + 64, pa1, pb1);
+#pragma unroll
+  for (int pc = 0; pc < 4; ++pc) piece(buf0, buf0 + kWgTM * 64, kb0, pc, pa0, pb0);
+  fetch(kb0 + 128, pa0, pb0);
   __syncthreads();
+  const std::integral_constant<bool, true> with_stash;
+  const std::integral_constant<bool, false> no_stash;
   for (int c = 0; c < nchunk; c += 2) {
-    // even chunk c from buffer 0; chunk c+1 (set 1) -> buffer 1; set 1 <- chunk c+3
-    stash(As1, Bs1, ra1, rb1, kb0 + 64 * (c + 1));
-    fetch(kb0 + 64 * (c + 3), ra1, rb1);
-    compute(As0, Bs0);
+    // even chunk c from buf0, chunk c + 1 (set 1) -> buf1, set 1 <- chunk c + 3
+    if (c + 1 < nchunk) {
+      chunk(buf0, buf0 + kWgTM * 64, buf1, buf1 + kWgTM * 64, kb0 + 64 * (c + 1), pa1, pb1,
+            with_stash);
+      if (c + 3 < nchunk) fetch(kb0 + 64 * (c + 3), pa1, pb1);
+    } else {
+      chunk(buf0, buf0 + kWgTM * 64, buf1, buf1 + kWgTM * 64, 0, pa1, pb1, no_stash);
+    }
     __syncthreads();
     if (c + 1 >= nchunk) break;
-    // odd chunk c+1 from buffer 1; chunk c+2 (set 0) -> buffer 0; set 0 <- chunk c+4
-    stash(As0, Bs0, ra0, rb0, kb0 + 64 * (c + 2));
-    fetch(kb0 + 64 * (c + 4), ra0, rb0);
-    compute(As1, Bs1);
+    // odd chunk c + 1 from buf1, chunk c + 2 (set 0) -> buf0, set 0 <- chunk c + 4
+    if (c + 2 < nchunk) {
+      chunk(buf1, buf1 + kWgTM * 64, buf0, buf0 + kWgTM * 64, kb0 + 64 * (c + 2), pa0, pb0,
+            with_stash);
+      if (c + 4 < nchunk) fetch(kb0 + 64 * (c + 4), pa0, pb0);
+    } else {
+      chunk(buf1, buf1 + kWgTM * 64, buf0, buf0 + kWgTM * 64, 0, pa0, pb0, no_stash);
+    }
     __syncthreads();
   }
   PSEC(8);
-  // partial tile (+ bias column sums) -> slab; ppo_wsum adds the splits
-  float* slab = a.slab + ((long)tile_id * a.split + z) * (64 * 64 + 64);
+  // waves 4-7 hand their accumulators to waves 0-3 through LDS (fixed order: even + odd groups)
+  float* xch = wg_lds;  // [4 waves][32 floats][64 lanes]
+  if (kh == 1) {
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int ri = wm + (q & 3) + 8 * (q >> 2) + 4 * h;
-    slab[ri * 64 + wn + l32] = acc[q];
+    for (int q = 0; q < 16; ++q) {
+      xch[(wq * 32 + q) * 64 + lane] = acc0[q];
+      xch[(wq * 32 + 16 + q) * 64 + lane] = acc1[q];
+    }
   }
-  if (t < 64) slab[64 * 64 + t] = bsum;
+  // bias partials of the 8 (w, ra) row sets per feature
+  float* bpart = wg_lds + 4 * 32 * 64;  // [16][128]
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bpart[(2 * w + ra) * kWgTM + 4 * ca + i] = bsum[i];
+  __syncthreads();
+  float* part = a.slab + ((long)tile_id * a.split + z) * kWgPart;
+  if (kh == 0) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int ri = wm + (q & 3) + 8 * (q >> 2) + 4 * h;
+      part[ri * kWgTN + wn + l32] = acc0[q] + xch[(wq * 32 + q) * 64 + lane];
+      part[(ri + 32) * kWgTN + wn + l32] = acc1[q] + xch[(wq * 32 + 16 + q) * 64 + lane];
+    }
+  } else if (tj == 0 && t - 256 < kWgTM) {
+    const int f = t - 256;
+    float v = 0.0f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v += bpart[r * kWgTM + f];
+    part[kWgTM * kWgTN + f] = v;
+  }
   PSEC(9);
   PSEC_FLUSH;
 }
 
-// ppo_wsum: the `split` partial tiles of every weight-gradient tile summed in split order
-// (deterministic) into the flat gradient, one quarter tile per workgroup (4 elements x all
-// splits in flight per thread), plus the bias sums and a sum-of-squares partial each.
+// ppo_wsum: the split partial tiles of every weight-gradient tile summed in split order
+// (deterministic) into the flat gradient, 1024 elements (16 tile rows) per workgroup with all
+// splits' float4s in flight per thread, the bias sums, and one sum-of-squares partial each.
 __global__ void __launch_bounds__(256) ppo_wsum(WgArgs a) {
   __shared__ float red[4];
   const int t = threadIdx.x, H = a.H;
-  const int tile_id = blockIdx.x >> 2, quarter = blockIdx.x & 3;
-  int id = tile_id, ntj, N, region;
+  constexpr int kParts = kWgTM * kWgTN / 1024;
+  const int tile_id = blockIdx.x / kParts, part = blockIdx.x % kParts;
+  int id = tile_id, M, N, region;
   if (id < a.tac) {
-    ntj = H / 64, N = H, region = 0;
+    M = 2 * H, N = H, region = 0;
   } else if (id < a.tac + a.t2) {
-    id -= a.tac, ntj = H / 64, N = H, region = 1;
+    id -= a.tac, M = H, N = H, region = 1;
   } else {
-    id -= a.tac + a.t2, ntj = (a.S + 63) / 64, N = a.S, region = 2;
+    id -= a.tac + a.t2, M = H, N = a.S, region = 2;
   }
-  const int ti = id / ntj, tj = id % ntj, i0 = ti * 64, j0 = tj * 64;
-  long base, bbase;
-  int ldo;
-  if (region == 0) {  // dWac rows -> Wa1 / Wc1
-    base = i0 < H ? a.off[P_WA1] + (long)i0 * H : a.off[P_WC1] + (long)(i0 - H) * H;
-    bbase = i0 < H ? a.off[P_BA1] + i0 : a.off[P_BC1] + (i0 - H);
-    ldo = H;
-  } else if (region == 1) {
-    base = a.off[P_W2] + (long)i0 * H, bbase = a.off[P_B2] + i0, ldo = H;
-  } else {
-    base = a.off[P_W1] + (long)i0 * a.S, bbase = a.off[P_B1] + i0, ldo = a.S;
-  }
-  const float* sl = a.slab + (long)tile_id * a.split * (64 * 64 + 64);
+  const int ntj = (N + kWgTN - 1) / kWgTN;
+  const int ti = id / ntj, tj = id % ntj, i0 = ti * kWgTM, j0 = tj * kWgTN;
+  auto grad_row = [&](int i) -> long {  // flat index of row i (of M) of this region's weight
+    if (region == 0) return i < H ? a.off[P_WA1] + (long)i * H : a.off[P_WC1] + (long)(i - H) * H;
+    if (region == 1) return a.off[P_W2] + (long)i * H;
+    return a.off[P_W1] + (long)i * a.S;
+  };
+  const float* sl = a.slab + (long)tile_id * a.split * kWgPart;
+  const int e = part * 1024 + 4 * t, ri = e / kWgTN, cj = e % kWgTN;
   constexpr int kMaxSplit = 8;
-  float pv[4][kMaxSplit];
+  f32x4 pv[kMaxSplit];
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int zz = 0; zz < kMaxSplit; ++zz)
+    if (zz < a.split) pv[zz] = *reinterpret_cast<const f32x4*>(sl + (long)zz * kWgPart + e);
+  f32x4 v = pv[0];
 #pragma unroll
-    for (int zz = 0; zz < kMaxSplit; ++zz)
-      pv[q][zz] = zz < a.split ? sl[(long)zz * (64 * 64 + 64) + quarter * 1024 + t + 256 * q]
-                               : 0.0f;
+  for (int zz = 1; zz < kMaxSplit; ++zz)
+    if (zz < a.split) v += pv[zz];
   float sq = 0.0f;
+  if (i0 + ri < M) {
+    float* dst = a.grads + grad_row(i0 + ri) + j0 + cj;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int e = quarter * 1024 + t + 256 * q, ri = e >> 6, cj = e & 63;
-    float v = pv[q][0];
-#pragma unroll
-    for (int zz = 1; zz < kMaxSplit; ++zz)
-      if (zz < a.split) v += pv[q][zz];
-    if (j0 + cj < N) {
-      a.grads[base + (long)ri * ldo + j0 + cj] = v;
-      sq += v * v;
-    }
+    for (int c4 = 0; c4 < 4; ++c4)
+      if (j0 + cj + c4 < N) {
+        dst[c4] = v[c4];
+        sq += v[c4] * v[c4];
+      }
   }
-  if (quarter == 0 && tj == 0 && t < 64) {  // bias = column sum of the output-gradient matrix
-    float v = 0.0f;
-    for (int zz = 0; zz < a.split; ++zz) v += sl[(long)zz * (64 * 64 + 64) + 64 * 64 + t];
-    a.grads[bbase + t] = v;
-    sq += v * v;
+  if (part == 0 && tj == 0 && t < kWgTM && i0 + t < M) {  // bias of output row i0 + t
+    float b = 0.0f;
+    for (int zz = 0; zz < a.split; ++zz) b += sl[(long)zz * kWgPart + kWgTM * kWgTN + t];
+    const int i = i0 + t;
+    long bo;
+    if (region == 0) bo = i < H ? a.off[P_BA1] + i : a.off[P_BC1] + (i - H);
+    else if (region == 1) bo = a.off[P_B2] + i;
+    else bo = a.off[P_B1] + i;
+    a.grads[bo] = b;
+    sq += b * b;
   }
   const float tot = block_sum4(sq, red);
   if (t == 0) a.norm_part[a.nh + blockIdx.x] = tot;
@@ -1761,9 +1880,9 @@ int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
     g.entropy_coef = a->entropy_coef, g.value_coef = a->value_coef;
     g.ent_const = 0.5f + 0.91893853320467274178f;
     g.params = P, g.metrics = a->metrics, g.counters = a->counters;
-    hipLaunchKernelGGL(ppo_wgrad, dim3(w.grid2), blk, 0, s, g);
+    hipLaunchKernelGGL(ppo_wgrad, dim3(w.grid2), dim3(64 * kWgWaves), 0, s, g);
     rc |= hipGetLastError() == hipSuccess ? 0 : -1;
-    hipLaunchKernelGGL(ppo_wsum, dim3(4 * (w.tac + w.t2 + w.t1)), blk, 0, s, g);
+    hipLaunchKernelGGL(ppo_wsum, dim3((w.tac + w.t2 + w.t1) * (kWgTM * kWgTN / 1024)), blk, 0, s, g);
     rc |= hipGetLastError() == hipSuccess ? 0 : -1;
     return rc;
   }

@@ -46,8 +46,9 @@ names = {0: "rows: gather", 1: "rows: h1", 2: "rows: h2", 3: "rows: ac", 7: "row
 tot = sum(buf[i] for i in names)
 for i, nm in names.items():
     print(f"  {nm:22s} {buf[i] / (steps * n1):10,.0f} clk/WG  {100 * buf[i] / tot:5.1f}%")
-ntile = (2 * H // 64) * (H // 64) + (H // 64) ** 2 + (H // 64) * ((S + 63) // 64)
-split = max(1, min(8, 512 // ntile, (mb + 63) // 64))
+tm, tn = (H + 127) // 128, (H + 63) // 64  # 128x64 ppo_wgrad tiles
+ntile = ((2 * H + 127) // 128) * tn + tm * tn + tm * ((S + 63) // 64)
+split = max(1, min(8, 256 // ntile, (mb + 63) // 64))
 nh = (3 * H + 9 + 63) // 64
 print(f"  wgrad tiles={ntile} split={split} head WGs={nh}")
 print(f"  {'wgrad: chunk loop':22s} {buf[8] / (steps * ntile * split):10,.0f} clk/WG")
