@@ -1316,6 +1316,11 @@ __device__ void wgrad_head(const WgArgs& a, int hid, float* lds, float* red) {
   }
 }
 
+#ifdef HWY_WG_NT
+#define WG_ST(p, v) __builtin_nontemporal_store((v), (p))
+#else
+#define WG_ST(p, v) (*(p) = (v))
+#endif
 __global__ void __launch_bounds__(512) ppo_wgrad(WgArgs a) {
   PSEC_DECL
   __shared__ __attribute__((aligned(16))) float wg_lds[2 * (kWgTM + kWgTN) * 64];
@@ -1498,15 +1503,15 @@ __global__ void __launch_bounds__(512) ppo_wgrad(WgArgs a) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int ri = wm + (q & 3) + 8 * (q >> 2) + 4 * h;
-      part[ri * kWgTN + wn + l32] = acc0[q] + xch[(wq * 32 + q) * 64 + lane];
-      part[(ri + 32) * kWgTN + wn + l32] = acc1[q] + xch[(wq * 32 + 16 + q) * 64 + lane];
+      WG_ST(&part[ri * kWgTN + wn + l32], acc0[q] + xch[(wq * 32 + q) * 64 + lane]);
+      WG_ST(&part[(ri + 32) * kWgTN + wn + l32], acc1[q] + xch[(wq * 32 + 16 + q) * 64 + lane]);
     }
   } else if (tj == 0 && t - 256 < kWgTM) {
     const int f = t - 256;
     float v = 0.0f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) v += bpart[r * kWgTM + f];
-    part[kWgTM * kWgTN + f] = v;
+    WG_ST(&part[kWgTM * kWgTN + f], v);
   }
   PSEC(9);
   PSEC_FLUSH;

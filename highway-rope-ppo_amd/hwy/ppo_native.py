@@ -122,10 +122,12 @@ def act_supported(S: int, H: int, A: int) -> bool:
 
 
 def fused_act(agent, states: torch.Tensor, deterministic: bool = False,
-              generator: Optional[torch.Generator] = None):
+              generator: Optional[torch.Generator] = None, out=None):
     """ActorCritic.act (ppo/agent.py:86-95) through hwy_ppo_act: one launch for the forward,
     the Normal sample (noise drawn from `generator` exactly as act() draws it), tanh and the
-    squashed log-prob.  Returns (action, pre_tanh, log_prob, value)."""
+    squashed log-prob.  Returns (action, pre_tanh, log_prob, value); `out` = four contiguous
+    float32 device tensors of shapes (B, 2), (B, 2), (B,), (B,) to write them into instead
+    (e.g. the rollout buffer rows of this step)."""
     flat = flat_params(agent)[0]
     B, S = states.shape
     H = agent.actor_critic.shared[0].weight.shape[0]
@@ -134,10 +136,17 @@ def fused_act(agent, states: torch.Tensor, deterministic: bool = False,
     noise = None
     if not deterministic:
         noise = torch.randn((B, 2), device=dev, dtype=states.dtype, generator=generator)
-    action = torch.empty(B, 2, device=dev)
-    pre = torch.empty(B, 2, device=dev)
-    logp = torch.empty(B, device=dev)
-    value = torch.empty(B, device=dev)
+    if out is None:
+        action = torch.empty(B, 2, device=dev)
+        pre = torch.empty(B, 2, device=dev)
+        logp = torch.empty(B, device=dev)
+        value = torch.empty(B, device=dev)
+    else:
+        action, pre, logp, value = out
+        for t, shp in zip(out, ((B, 2), (B, 2), (B,), (B,))):
+            if (tuple(t.shape) != shp or t.dtype != torch.float32 or t.device != dev
+                    or not t.is_contiguous()):
+                raise ValueError(f"fused_act out tensor must be contiguous float32 {shp} on {dev}")
     a = PpoActArgs()
     a.dims = PpoDims(B, S, H, 2)
     a.states, a.params = states.data_ptr(), flat.data_ptr()
@@ -181,6 +190,9 @@ class FusedPPO:
         self._import_torch_state()
         self._graphs = None
         self._bound_key = None
+        # when a list: (start, end) HIP events on the launch stream around every epoch's
+        # minibatch steps are appended to it (bench.py's live timing of the update)
+        self.epoch_events: Optional[list] = None
 
     # -------------------------------------------------------------- optimizer state <-> torch
     def _import_torch_state(self):
@@ -270,6 +282,7 @@ class FusedPPO:
             self._capture(args)
             self._bound_key = key
         for _ in range(epochs):
+            ev = self._epoch_event()
             if self.group is None:
                 self._graphs[0].replay()
             else:
@@ -277,7 +290,17 @@ class FusedPPO:
                     gf.replay()
                     self._allreduce()
                     go.replay()
+            self._epoch_event(ev)
         return self.metrics
+
+    def _epoch_event(self, start=None):
+        if self.epoch_events is None:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(torch.cuda.current_stream())
+        if start is not None:
+            self.epoch_events.append((start, e))
+        return e
 
     def _capture(self, args):
         self._keep_args = args

@@ -339,13 +339,20 @@ class PPOAgent:
             self.generator.manual_seed(int(seed) if seed is not None else torch.initial_seed() % (2**63))
 
     # ------------------------------------------------------------------ acting
-    def select_action(self, state, deterministic: bool = False):
+    def select_action(self, state, deterministic: bool = False, out=None):
+        """Batched (2-D tensor) or single-state acting.  For a batch, `out` may name the four
+        tensors (action, pre_tanh, log_prob, value) to write, e.g. a rollout buffer's rows."""
         if isinstance(state, torch.Tensor) and state.dim() == 2:
             if self._act_fused_ok(state):
                 from hwy.ppo_native import fused_act
 
-                return fused_act(self, state, deterministic, self.generator)
-            return self.actor_critic.act(state, deterministic, generator=self.generator)
+                return fused_act(self, state, deterministic, self.generator, out=out)
+            res = self.actor_critic.act(state, deterministic, generator=self.generator)
+            if out is None:
+                return res
+            for dst, src in zip(out, res):
+                dst.copy_(src.reshape(dst.shape))
+            return tuple(out)
         return self.actor_critic.get_action(state, deterministic)
 
     def _act_fused_ok(self, state: torch.Tensor) -> bool:

@@ -293,11 +293,8 @@ def _train_vector(env, agent, max_episodes, log_interval, eval_interval, steps_p
     while episode_num < max_episodes:
         t_update = time.time()
         for t in range(T):
-            a, z, lp, v = agent.select_action(buf.states[t])
-            buf.actions[t].copy_(a)
-            buf.pre_tanh[t].copy_(z)
-            buf.log_probs[t].copy_(lp)
-            buf.values[t].copy_(v)
+            agent.select_action(buf.states[t], out=(buf.actions[t], buf.pre_tanh[t],
+                                                    buf.log_probs[t], buf.values[t]))
             base.step_into(buf.actions[t], buf.states[t + 1].view(E, *base.obs_buf.shape[1:]),
                            buf.rewards[t], buf.terminated[t], buf.truncated[t],
                            buf.ep_return[t], buf.ep_length[t])
