@@ -825,8 +825,24 @@ __device__ __forceinline__ void row_epi_mask(const f32x4 (&acc)[QH], float* mask
       const int row = 4 * g + r;
       const float v = mask_inout[row * pm + n] > 0.0f ? acc[t][r] : 0.0f;
       if (write_lds) mask_inout[row * pm + n] = v;
-      if (row < nrows) gout[(long)row * ldg + n] = v;
+      if (gout && row < nrows) gout[(long)row * ldg + n] = v;
     }
+  }
+}
+
+// 16-B store of a row-kernel output (write-through sc1 stores measured no faster here)
+__device__ __forceinline__ void st_f4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+
+// rows 0 .. nrows-1 of an LDS image (pitch floats, ncols % 4 == 0) to HBM rows of ldg floats:
+// whole 16-B segments, consecutive lanes on consecutive segments of a row
+template <int NT>
+__device__ __forceinline__ void rows_out(const float* img, int pitch, float* g, int ldg, int ncols,
+                                         int nrows) {
+  const int per_row = ncols / 4;
+  for (int e = threadIdx.x; e < kRowTile * per_row; e += NT) {
+    const int row = e / per_row, c4 = (e - row * per_row) * 4;
+    if (row < nrows)
+      st_f4(g + (long)row * ldg + c4, *reinterpret_cast<const f32x4*>(&img[row * pitch + c4]));
   }
 }
 
@@ -874,16 +890,16 @@ __device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG, TL>& R
   // h1 = relu(x W1^T + b1)
   zero_acc(acc);
   R.template run<0>(X, px, acc);
-  row_epi_bias_relu<TW>(acc, bias[0], H1, PH, h1g ? h1g + (long)row0 * H : nullptr, H,
-                        nrows, nb);
+  row_epi_bias_relu<TW>(acc, bias[0], H1, PH, nullptr, H, nrows, nb);
   __syncthreads();
+  if (h1g) rows_out<NT>(H1, PH, h1g + (long)row0 * H, H, H, nrows);
   PSEC(1);
   // h2 = relu(h1 W2^T + b2)
   zero_acc(acc);
   R.template run<1>(H1, PH, acc);
-  row_epi_bias_relu<TW>(acc, bias[1], H2, PH, h2g ? h2g + (long)row0 * H : nullptr, H,
-                        nrows, nb);
+  row_epi_bias_relu<TW>(acc, bias[1], H2, PH, nullptr, H, nrows, nb);
   __syncthreads();
+  if (h2g) rows_out<NT>(H2, PH, h2g + (long)row0 * H, H, H, nrows);
   PSEC(2);
   // [a1 | c1] = relu(h2 [Wa1; Wc1]^T + [ba1; bc1])
   zero_acc(acc);
@@ -1068,8 +1084,9 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   zero_acc(acc);
   R.template run<4>(AC, PA, acc);
   R.template run<5>(AC + H, PA, acc);
-  row_epi_mask<TW>(acc, H2, PH, true, r.dh2 + (long)row0 * H, H, nrows, nb);
+  row_epi_mask<TW>(acc, H2, PH, true, nullptr, H, nrows, nb);
   __syncthreads();
+  if (r.dh2) rows_out<NT>(H2, PH, r.dh2 + (long)row0 * H, H, H, nrows);
   PSEC(5);
   // the head partials of the NW waves -> one row per workgroup (fixed order); [a1|c1] is free
   {
@@ -1098,7 +1115,9 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   // dh1 = (dh2 W2) * (h1 > 0)
   zero_acc(acc);
   R.template run<6>(H2, PH, acc);
-  row_epi_mask<TW>(acc, H1, PH, false, r.dh1 + (long)row0 * H, H, nrows, nb);
+  row_epi_mask<TW>(acc, H1, PH, true, nullptr, H, nrows, nb);  // dh1 over h1 (same thread)
+  __syncthreads();
+  if (r.dh1) rows_out<NT>(H1, PH, r.dh1 + (long)row0 * H, H, H, nrows);
   PSEC(6);
   PSEC_FLUSH;
 }
