@@ -253,11 +253,14 @@ class FusedPPO:
 
     def _allreduce(self):
         if self._avg_op:  # RCCL averages in the collective (no extra division kernel)
-            torch.distributed.all_reduce(self.grads, op=torch.distributed.ReduceOp.AVG,
-                                         group=self.group)
-        else:
-            torch.distributed.all_reduce(self.grads, group=self.group)
-            self.grads.div_(self.world)
+            try:
+                torch.distributed.all_reduce(self.grads, op=torch.distributed.ReduceOp.AVG,
+                                             group=self.group)
+                return
+            except RuntimeError:  # a collective library without ncclAvg: sum, then divide
+                self._avg_op = False
+        torch.distributed.all_reduce(self.grads, group=self.group)
+        self.grads.div_(self.world)
 
     def run(self, states, pre_tanh, old_lp, adv, ret, perm: torch.Tensor) -> torch.Tensor:
         """All epochs of one update; returns the [epochs*nmb, 6] metrics rows (device)."""
