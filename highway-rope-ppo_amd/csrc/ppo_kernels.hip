@@ -65,6 +65,9 @@ constexpr int kKStep = 32;
 constexpr int kHeadRows = 16;  // minibatch rows per head workgroup (4 per wave)
 constexpr int kRowTile = 16;   // minibatch rows per ppo_rows workgroup
 constexpr int kMaxRowS = 256;  // states dim bound of the fused path (LDS)
+#ifndef HWY_ROWS_NW
+#define HWY_ROWS_NW 8  // ppo_rows waves at H = 256 (16: 4 per SIMD, one 16-column tile each)
+#endif
 constexpr int kWgTM = 128, kWgTN = 64;          // ppo_wgrad output tile
 constexpr int kWgWaves = 8;                     // ppo_wgrad waves (2 per SIMD)
 constexpr int kWgPart = kWgTM * kWgTN + kWgTM;  // floats per partial tile (+ bias sums)
@@ -920,11 +923,15 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   constexpr int WPS = 3 * H + 16;        // per-wave head-partial stride (LDS)
   static_assert(TW * 16 * NW == H, "H must split into 16-column tiles per wave");
   constexpr int PH = H + 4, PA = 2 * H + 4, PXMAX = kMaxRowS + 4;
-  static_assert(NW * WPS <= kRowTile * PA, "head partials must fit the [a1|c1] image");
+  // the waves' head partials are combined in the [a1|c1] image (free by then), or in a separate
+  // array when NW waves' partials do not fit it
+  constexpr bool kOwnHP = NW * WPS > kRowTile * PA;
   __shared__ __attribute__((aligned(16))) float X[kRowTile * PXMAX];
   __shared__ __attribute__((aligned(16))) float H1[kRowTile * PH];
   __shared__ __attribute__((aligned(16))) float H2[kRowTile * PH];
   __shared__ __attribute__((aligned(16))) float AC[kRowTile * PA];
+  __shared__ float HPX[kOwnHP ? NW * WPS : 1];
+  float* HPW = kOwnHP ? HPX : AC;
   PSEC_DECL
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int S = r.S;
@@ -1090,7 +1097,7 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   PSEC(5);
   // the head partials of the NW waves -> one row per workgroup (fixed order); [a1|c1] is free
   {
-    float* wp = AC + w * WPS;
+    float* wp = HPW + w * WPS;
 #pragma unroll
     for (int q = 0; q < QH; ++q) {
       const int col = lane + 64 * q;
@@ -1106,9 +1113,9 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
     __syncthreads();
     float* out = r.head_part + (long)blockIdx.x * r.HP;
     for (int j = t; j < 3 * H + 9; j += NT) {
-      float v = AC[j];
+      float v = HPW[j];
 #pragma unroll
-      for (int ww = 1; ww < NW; ++ww) v += AC[ww * WPS + j];
+      for (int ww = 1; ww < NW; ++ww) v += HPW[ww * WPS + j];
       out[j] = v;
     }
   }
@@ -1882,7 +1889,7 @@ int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
       case 1: hipLaunchKernelGGL((ppo_rows<1, 4>), g1, b4, 0, s, r); break;
       case 2: hipLaunchKernelGGL((ppo_rows<2, 8>), g1, b8, 0, s, r); break;
       case 3: hipLaunchKernelGGL((ppo_rows<3, 4>), g1, b4, 0, s, r); break;
-      case 4: hipLaunchKernelGGL((ppo_rows<4, 8>), g1, b8, 0, s, r); break;
+      case 4: hipLaunchKernelGGL((ppo_rows<4, HWY_ROWS_NW>), g1, dim3(64 * HWY_ROWS_NW), 0, s, r); break;
       case 5: hipLaunchKernelGGL((ppo_rows<5, 4>), g1, b4, 0, s, r); break;
       case 6: hipLaunchKernelGGL((ppo_rows<6, 8>), g1, b8, 0, s, r); break;
       case 7: hipLaunchKernelGGL((ppo_rows<7, 4>), g1, b4, 0, s, r); break;
