@@ -1140,9 +1140,10 @@ struct ActArgs {
   int64_t off[13];
   const float* noise;  // [B][2] standard normal, or null
   float *action, *pre_tanh, *logp, *value;
+  const float* tiles;  // weight tile image in step with params (TL), else null
 };
 
-template <int QH, int NW>
+template <int QH, int NW, bool TL>
 __global__ void __launch_bounds__(64 * NW, 1) ppo_act(ActArgs r) {
   constexpr int H = 64 * QH;
   constexpr int RPW = kRowTile / NW;
@@ -1157,8 +1158,8 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_act(ActArgs r) {
   const float* P = r.params;
   constexpr int TW = H_TW(QH, NW);
   constexpr int D = ring_depth<TW>();
-  WRing<TW, D, 4, false> R;
-  ring_setup(R, P, r.off, r.S, H, w * (H / NW), nullptr);
+  WRing<TW, D, 4, TL> R;
+  ring_setup(R, P, r.off, r.S, H, w * (H / NW), r.tiles);
   R.prime();
 #ifdef HWY_SECTION_PROFILE
   uint64_t _pt = 0, _pacc[16];
@@ -1862,6 +1863,13 @@ int64_t hwy_ppo_workspace_bytes(const hwy_ppo_dims* d) {
   return bytes;
 }
 
+int64_t hwy_ppo_tile_image_offset(const hwy_ppo_dims* d) {
+  if (hwy_ppo_workspace_bytes(d) < 0 || !fused_ok(*d)) return -1;
+  char* base = reinterpret_cast<char*>(uintptr_t(1) << 20);  // carve only adds offsets to it
+  const Work w = carve(*d, base, nullptr);
+  return (int64_t)(reinterpret_cast<char*>(w.wtile) - base);
+}
+
 int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
   if (!a) return -1;
   const hwy_ppo_dims& d = a->dims;
@@ -2085,17 +2093,25 @@ int hwy_ppo_act(const hwy_ppo_act_args* a, void* stream) {
   r.B = d.B, r.S = d.S, r.states = a->states, r.params = a->params, r.noise = a->noise;
   for (int i = 0; i < 13; ++i) r.off[i] = L.off[i];
   r.action = a->action, r.pre_tanh = a->pre_tanh, r.logp = a->logp, r.value = a->value;
+  r.tiles = a->tiles;
   const dim3 g((d.B + kRowTile - 1) / kRowTile), b4(256), b8(512);
-  switch (d.H / 64) {
-    case 1: hipLaunchKernelGGL((ppo_act<1, 4>), g, b4, 0, s, r); break;
-    case 2: hipLaunchKernelGGL((ppo_act<2, 8>), g, b8, 0, s, r); break;
-    case 3: hipLaunchKernelGGL((ppo_act<3, 4>), g, b4, 0, s, r); break;
-    case 4: hipLaunchKernelGGL((ppo_act<4, 8>), g, b8, 0, s, r); break;
-    case 5: hipLaunchKernelGGL((ppo_act<5, 4>), g, b4, 0, s, r); break;
-    case 6: hipLaunchKernelGGL((ppo_act<6, 8>), g, b8, 0, s, r); break;
-    case 7: hipLaunchKernelGGL((ppo_act<7, 4>), g, b4, 0, s, r); break;
-    default: hipLaunchKernelGGL((ppo_act<8, 8>), g, b8, 0, s, r); break;
-  }
+  auto launch = [&](auto tl) {
+    constexpr bool TL = decltype(tl)::value;
+    switch (d.H / 64) {
+      case 1: hipLaunchKernelGGL((ppo_act<1, 4, TL>), g, b4, 0, s, r); break;
+      case 2: hipLaunchKernelGGL((ppo_act<2, 8, TL>), g, b8, 0, s, r); break;
+      case 3: hipLaunchKernelGGL((ppo_act<3, 4, TL>), g, b4, 0, s, r); break;
+      case 4: hipLaunchKernelGGL((ppo_act<4, 8, TL>), g, b8, 0, s, r); break;
+      case 5: hipLaunchKernelGGL((ppo_act<5, 4, TL>), g, b4, 0, s, r); break;
+      case 6: hipLaunchKernelGGL((ppo_act<6, 8, TL>), g, b8, 0, s, r); break;
+      case 7: hipLaunchKernelGGL((ppo_act<7, 4, TL>), g, b4, 0, s, r); break;
+      default: hipLaunchKernelGGL((ppo_act<8, 8, TL>), g, b8, 0, s, r); break;
+    }
+  };
+  if (r.tiles)
+    launch(std::integral_constant<bool, true>());
+  else
+    launch(std::integral_constant<bool, false>());
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

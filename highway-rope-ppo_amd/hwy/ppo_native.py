@@ -50,7 +50,7 @@ class PpoActArgs(ctypes.Structure):
         ("dims", PpoDims),
         ("states", ctypes.c_void_p), ("params", ctypes.c_void_p), ("noise", ctypes.c_void_p),
         ("action", ctypes.c_void_p), ("pre_tanh", ctypes.c_void_p), ("logp", ctypes.c_void_p),
-        ("value", ctypes.c_void_p),
+        ("value", ctypes.c_void_p), ("tiles", ctypes.c_void_p),
     ]
 
 
@@ -69,6 +69,8 @@ def _bind(L):
     L.hwy_ppo_sync_params.restype = ctypes.c_int
     L.hwy_ppo_act.argtypes = [ctypes.POINTER(PpoActArgs), ctypes.c_void_p]
     L.hwy_ppo_act.restype = ctypes.c_int
+    L.hwy_ppo_tile_image_offset.argtypes = [ctypes.POINTER(PpoDims)]
+    L.hwy_ppo_tile_image_offset.restype = ctypes.c_int64
     L._ppo_bound = True
     return L
 
@@ -153,6 +155,8 @@ def fused_act(agent, states: torch.Tensor, deterministic: bool = False,
     a.noise = None if noise is None else noise.data_ptr()
     a.action, a.pre_tanh, a.logp, a.value = (action.data_ptr(), pre.data_ptr(), logp.data_ptr(),
                                              value.data_ptr())
+    F = getattr(agent, "_fused", None)
+    a.tiles = F.current_tiles(flat) if F is not None else None
     check(_bind(lib()).hwy_ppo_act(ctypes.byref(a), stream_ptr()), "hwy_ppo_act")
     return action, pre, logp, value
 
@@ -193,6 +197,9 @@ class FusedPPO:
         # when a list: (start, end) HIP events on the launch stream around every epoch's
         # minibatch steps are appended to it (bench.py's live timing of the update)
         self.epoch_events: Optional[list] = None
+        off = L.hwy_ppo_tile_image_offset(ctypes.byref(self.dims))
+        self._tile_off = int(off) if off >= 0 else None
+        self._tiles_version = None  # flat._version when the tile image was last made current
 
     # -------------------------------------------------------------- optimizer state <-> torch
     def _import_torch_state(self):
@@ -251,6 +258,21 @@ class FusedPPO:
         needed before a step whenever params changed outside hwy_ppo_optimizer."""
         check(self.L.hwy_ppo_sync_params(ctypes.byref(a), stream_ptr()), "hwy_ppo_sync_params")
 
+    def current_tiles(self, flat: torch.Tensor) -> Optional[int]:
+        """Device address of the weight tile image when it is in step with `flat` (it is after
+        run(): hwy_ppo_optimizer rewrites it with the weights; any torch-side write to the
+        parameters since -- load_state_dict, a torch optimizer step -- bumps a version counter
+        and the caller reads params instead), else None."""
+        if (self._tile_off is None or flat is not self.flat
+                or self._tiles_version != self._param_versions()):
+            return None
+        return self.workspace.data_ptr() + self._tile_off
+
+    def _param_versions(self):
+        # in-place writes through a parameter (load_state_dict, a torch optimizer step) bump that
+        # parameter's counter, writes through the flat buffer bump the buffer's
+        return (self.flat._version,) + tuple(p._version for p in self.params)
+
     def _allreduce(self):
         if self._avg_op:  # RCCL averages in the collective (no extra division kernel)
             try:
@@ -280,6 +302,7 @@ class FusedPPO:
                     if self.group is not None:
                         self._allreduce()
                     self._opt(a)
+            self._tiles_version = self._param_versions()
             return self.metrics
         if self._graphs is None or self._bound_key != key:
             self._capture(args)
@@ -294,6 +317,7 @@ class FusedPPO:
                     self._allreduce()
                     go.replay()
             self._epoch_event(ev)
+        self._tiles_version = self._param_versions()
         return self.metrics
 
     def _epoch_event(self, start=None):

@@ -74,11 +74,18 @@ int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream);
 /* Rebuild the workspace's weight tile image from params (uses dims, params, workspace). */
 int hwy_ppo_sync_params(const hwy_ppo_args* a, void* stream);
 
+/* Byte offset of the weight tile image inside a workspace for dims (-1 when the dims take
+ * the general path, which keeps none).  The image depends on S and H only. */
+int64_t hwy_ppo_tile_image_offset(const hwy_ppo_dims* d);
+
 /* ActorCritic.act on a batch (replaces ppo/agent.py:86-95's forward + Normal sample + tanh +
  * squashed log-prob on the batched rollout path): dims.B rows of states [B][S] (contiguous);
  * noise [B][2] standard-normal draws (the caller's generator, as act() draws them) or NULL for
  * act(deterministic=True) (z = mean, log_prob = 0).  Needs S % 4 == 0, S <= 256,
- * H in {64, 128, ..., 512}. */
+ * H in {64, 128, ..., 512}.  tiles: NULL, or the tile image of a hwy_ppo workspace with the same
+ * S and H that is in step with params (workspace + hwy_ppo_tile_image_offset; current after
+ * hwy_ppo_optimizer / hwy_ppo_sync_params until params are written by anything else): the
+ * forward then streams whole 1-KB operand tiles instead of 64-B pieces of params rows. */
 typedef struct hwy_ppo_act_args {
   hwy_ppo_dims dims;
   const float* states;
@@ -88,6 +95,7 @@ typedef struct hwy_ppo_act_args {
   float* pre_tanh; /* [B][2] z */
   float* logp;     /* [B] */
   float* value;    /* [B] */
+  const float* tiles; /* optional weight tile image (see above), or NULL */
 } hwy_ppo_act_args;
 int hwy_ppo_act(const hwy_ppo_act_args* a, void* stream);
 

@@ -178,3 +178,37 @@ def test_fused_act_matches_actor_critic_act(S, H, B):
     b.generator = torch.Generator(device=DEV).manual_seed(3)
     out = b.select_action(s)
     assert out[0].shape == (B, 2) and bool(torch.all(out[0].abs() <= 1))
+
+
+@pytest.mark.parametrize("S,H", [(60, 256), (120, 192)])
+def test_fused_act_from_tile_image_equals_params_path(S, H):
+    """After a fused update the acting kernel streams the update's weight tile image
+    (hwy_ppo_tile_image_offset); results are bit-identical to reading the flat params, and a
+    torch-side parameter write (load_state_dict) retires the image until the next update."""
+    from hwy.ppo_native import fused_act
+
+    a, b = _agents(S, H)
+    n, nmb = 1024, 4
+    s, z, lp, adv, ret, perm = _data(n, S, a)
+    F = FusedPPO(b, n // nmb, nmb, use_graphs=False)
+    b._fused = F
+    F.run(s, z, lp, adv.clone(), ret.clone(), perm.clone())
+    flat = F.flat
+    assert F.current_tiles(flat) is not None
+    x = torch.randn(777, S, device=DEV)
+    with torch.no_grad():
+        got_t = fused_act(b, x, generator=torch.Generator(device=DEV).manual_seed(5))
+        saved = F._tiles_version
+        F._tiles_version = None  # force the params path
+        got_p = fused_act(b, x, generator=torch.Generator(device=DEV).manual_seed(5))
+        F._tiles_version = saved
+    for t_, p_ in zip(got_t, got_p):
+        assert torch.equal(t_, p_)
+    # a torch-side write bumps the flat buffer's version: acting falls back to params
+    b.actor_critic.load_state_dict(a.actor_critic.state_dict())
+    assert F.current_tiles(flat) is None
+    with torch.no_grad():
+        ref = a.actor_critic.act(x, deterministic=True)
+        got = fused_act(b, x, deterministic=True)
+    for r, g in zip(ref, got):
+        torch.testing.assert_close(g, r, rtol=1e-4, atol=2e-5)
