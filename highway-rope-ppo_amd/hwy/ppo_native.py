@@ -13,6 +13,7 @@ forward used for acting see the same storage) and runs one update's minibatch st
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import List, Optional
 
 import torch
@@ -189,7 +190,12 @@ class FusedPPO:
         self.metrics = torch.zeros(max(1, agent.epochs * nmb), 6, device=dev)
         self.group = group
         self.world = 1 if group is None else torch.distributed.get_world_size(group)
-        self._avg_op = group is not None and torch.distributed.get_backend(group) == "nccl"
+        self._rccl = group is not None and torch.distributed.get_backend(group) == "nccl"
+        self._avg_op = self._rccl
+        # RCCL collectives are captured into the epoch graph with the kernels (one replay per
+        # epoch, as on one GPU); HWY_GRAPH_COLLECTIVES=0 keeps them between per-step graphs
+        self.capture_collectives = self._rccl and os.environ.get("HWY_GRAPH_COLLECTIVES", "1") != "0"
+        self._captured_collectives = False
         self.use_graphs = use_graphs
         self._import_torch_state()
         self._graphs = None
@@ -309,7 +315,7 @@ class FusedPPO:
             self._bound_key = key
         for _ in range(epochs):
             ev = self._epoch_event()
-            if self.group is None:
+            if self.group is None or self._captured_collectives:
                 self._graphs[0].replay()
             else:
                 for gf, go in self._graphs:
@@ -331,6 +337,8 @@ class FusedPPO:
 
     def _capture(self, args):
         self._keep_args = args
+        if self.capture_collectives and self._capture_with_collectives(args):
+            return
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         graphs = []
@@ -352,3 +360,31 @@ class FusedPPO:
                     graphs.append((gf, go))
         torch.cuda.current_stream().wait_stream(s)
         self._graphs = graphs
+        self._captured_collectives = False
+
+    def _capture_with_collectives(self, args) -> bool:
+        """One graph per epoch holding every step's forward/backward, the RCCL gradient
+        all-reduce and the optimizer (the communicator is warmed up, and the AVG op probed,
+        outside the capture).  False when the capture is refused: the caller falls back to
+        per-step graphs with the all-reduce between them."""
+        self._allreduce()  # communicator set-up + AVG support, before any capture
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.stream(s):
+                # thread_local: the process group's watchdog thread may query events meanwhile
+                with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+                    for a in args:
+                        self._fwd_bwd(a)
+                        self._allreduce()
+                        self._opt(a)
+        except RuntimeError:
+            torch.cuda.synchronize()
+            self.capture_collectives = False
+            return False
+        torch.cuda.current_stream().wait_stream(s)
+        self._graphs = [g]
+        self._captured_collectives = True
+        return True

@@ -90,3 +90,50 @@ def test_fused_sharded_update_equals_single_process(tmp_path):
         # element by up to ~lr per step: bound the worst case, require nearly all to agree
         assert dd.max().item() <= 2 * 3e-4 * steps, k
         assert (dd > 2e-5).float().mean().item() < 0.05, (k, dd.max().item())
+
+
+def _rccl1_worker(rank, port, out_dir):
+    """1-rank RCCL group: the epoch graph with the all-reduce captured, the per-step graphs with
+    the all-reduce between them, and no process group must give the same weights."""
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.join(os.path.dirname(here), "highway-rope-ppo_amd"), here]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    torch.distributed.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    from hwy.ppo_native import FusedPPO
+
+    d = _data(0, dev)
+    out = {}
+    for tag, group, capture in (("captured", torch.distributed.group.WORLD, True),
+                                ("stepwise", torch.distributed.group.WORLD, False),
+                                ("local", None, False)):
+        agent = _agent(dev, group)
+        adv = agent.normalize_advantages(d["a"])
+        F = FusedPPO(agent, NLOC // NMB, NMB, group=group, use_graphs=True)
+        F.capture_collectives = capture
+        for _ in range(2):  # the second update replays the captured graphs
+            F.run(d["s"], d["z"].contiguous(), d["lp"], adv.contiguous(), d["r"], d["perm"])
+        torch.cuda.synchronize()
+        out[tag] = {"state": {k: v.cpu() for k, v in agent.actor_critic.state_dict().items()},
+                    "captured": F._captured_collectives}
+    torch.save(out, os.path.join(out_dir, "rccl1.pt"))
+    torch.distributed.destroy_process_group()
+
+
+def test_rccl_captured_allreduce_matches_stepwise_and_local(tmp_path):
+    port = _free_port()
+    mp.start_processes(_rccl1_worker, args=(port, str(tmp_path)), nprocs=1, join=True,
+                       start_method="spawn")
+    r = torch.load(tmp_path / "rccl1.pt", weights_only=True)
+    assert r["captured"]["captured"] and not r["stepwise"]["captured"]
+    for k in r["local"]["state"]:
+        # the captured graph replays exactly what the per-step path launches
+        torch.testing.assert_close(r["captured"]["state"][k], r["stepwise"]["state"][k], rtol=0,
+                                   atol=0)
+        # the group path recomputes clip_grad_norm_ from the reduced gradient (ppo_sumsq), whose
+        # partial sums round differently from ppo_wsum's
+        torch.testing.assert_close(r["captured"]["state"][k], r["local"]["state"][k], rtol=1e-4,
+                                   atol=1e-6)
