@@ -3,8 +3,8 @@
 
 Runs `ExperimentRunner.launch` (experiments/runner.py, the reference's runner sequence,
 /root/reference/experiments/runner.py:73-122) for the reference experiment
-`sorted_lr0.0003_hidden_dim256_clip_eps0.2_entropy_coef0.005_epochs8_batch_size64` at the given
-seeds, 1500 episodes, eval every 50 episodes, and compares `final_reward` (mean of the last 10
+`<condition>_lr0.0003_hidden_dim256_clip_eps0.2_entropy_coef0.005_epochs8_batch_size64` at the
+given seeds, 1500 episodes, eval every 50 episodes, and compares `final_reward` (mean of the last 10
 evals, each the mean of 5 deterministic episodes seeded exp_seed+1000+k;
 training/routine.py:181-186,292) with the reference's published value for the same seed
 (artifacts/combined_validated_data-final-run.csv rows sorted_..._hidden_dim256_..._batch_size64:
@@ -26,7 +26,14 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "highway-rope-ppo_amd"))
 
-REFERENCE_FINAL = {42: 136.8270, 1042: 127.8022, 2042: 132.6172}
+# artifacts/combined_validated_data-final-run.csv, lr 3e-4 / h256 / clip .2 / ent .005 / 8 epochs /
+# bs 64 (d_embed 4 for the PE conditions; the reference's own DistPE and RoPE rows coincide)
+REFERENCE_FINAL = {
+    "sorted": {42: 136.8270, 1042: 127.8022, 2042: 132.6172},
+    "shuffled_rope": {42: 136.0069, 1042: 82.4615, 2042: 125.5533},
+    "shuffled_distpe": {42: 136.0069, 1042: 82.4615, 2042: 125.5533},
+    "shuffled_rankpe": {42: 83.2977, 1042: 119.7457, 2042: 119.0862},
+}
 
 
 def main():
@@ -35,6 +42,7 @@ def main():
     p.add_argument("--episodes", type=int, default=1500)
     p.add_argument("--num-envs", type=int, default=1)
     p.add_argument("--out", default="gpurun_out/train")
+    p.add_argument("--condition", default="sorted", choices=sorted(REFERENCE_FINAL))
     args = p.parse_args()
 
     out = os.path.abspath(args.out)
@@ -46,17 +54,23 @@ def main():
     from experiments.runner import ExperimentRunner
 
     results = []
+    cond = {"sorted": Condition.SORTED, "shuffled_rope": Condition.SHUFFLED_ROPE,
+            "shuffled_distpe": Condition.SHUFFLED_DISTPE,
+            "shuffled_rankpe": Condition.SHUFFLED_RANKPE}[args.condition]
+    d_embed = None if args.condition == "sorted" else 4
     for seed in args.seeds:
-        name = ("sorted_lr0.0003_hidden_dim256_clip_eps0.2_entropy_coef0.005_epochs8_"
-                f"batch_size64_seed{seed}" + (f"_envs{args.num_envs}" if args.num_envs > 1 else ""))
-        hp = ConditionHP(lr=3e-4, clip_eps=0.2, epochs=8, batch_size=64, hidden_dim=256)
+        name = (f"{args.condition}_lr0.0003_hidden_dim256_clip_eps0.2_entropy_coef0.005_epochs8_"
+                f"batch_size64" + (f"_d_embed{d_embed}" if d_embed else "") + f"_seed{seed}"
+                + (f"_envs{args.num_envs}" if args.num_envs > 1 else ""))
+        hp = ConditionHP(lr=3e-4, clip_eps=0.2, epochs=8, batch_size=64, hidden_dim=256,
+                         d_embed=d_embed)
         hp.entropy_coef = 0.005
         extra = {"log_interval": 50, "eval_interval": 50}
         if args.num_envs > 1:
             extra["num_envs"] = args.num_envs
-        exp = Experiment(name=name, condition=Condition.SORTED, hp=hp, seed=seed,
+        exp = Experiment(name=name, condition=cond, hp=hp, seed=seed,
                          max_episodes=args.episodes, target_reward=130.0, extra=extra)
-        run_dir = os.path.join(out, f"seed{seed}")
+        run_dir = os.path.join(out, f"{args.condition}_seed{seed}")
         os.makedirs(run_dir, exist_ok=True)
         cwd = os.getcwd()
         os.chdir(run_dir)
@@ -66,7 +80,7 @@ def main():
         finally:
             os.chdir(cwd)
         wall = time.time() - t0
-        row = {"seed": seed, "experiment": name, "status": res["status"], "wall_s": round(wall, 1),
+        row = {"condition": args.condition, "seed": seed, "experiment": name, "status": res["status"], "wall_s": round(wall, 1),
                "num_envs": args.num_envs, "episodes": args.episodes,
                "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else "cpu"}
         if res["status"] == "COMPLETED":
@@ -74,7 +88,7 @@ def main():
             hist = res["metrics_history"]
             row.update(final_reward=round(float(avg[-1]), 4), max_reward=round(float(max(avg)), 4),
                        evals=[round(float(x), 2) for x in hist.get("eval_rewards", [])])
-            ref = REFERENCE_FINAL.get(seed)
+            ref = REFERENCE_FINAL[args.condition].get(seed)
             if ref is not None:
                 row.update(reference_final_reward=ref,
                            delta=round(float(avg[-1]) - ref, 4))
@@ -87,7 +101,10 @@ def main():
     done = [r for r in results if "final_reward" in r]
     if done:
         mean = sum(r["final_reward"] for r in done) / len(done)
-        print(json.dumps({"mean_final_reward": round(mean, 4), "reference_mean": 132.42,
+        refs = [REFERENCE_FINAL[args.condition][r["seed"]] for r in done
+                if r["seed"] in REFERENCE_FINAL[args.condition]]
+        print(json.dumps({"condition": args.condition, "mean_final_reward": round(mean, 4),
+                          "reference_mean": round(sum(refs) / len(refs), 4) if refs else None,
                           "n": len(done)}), flush=True)
 
 
