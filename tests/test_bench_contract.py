@@ -1,0 +1,38 @@
+"""bench.py's algorithmic-work figures and CLI defaults."""
+
+import importlib.util
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)  # defines functions only; main() runs under __main__
+    return m
+
+
+def test_env_step_algorithmic_bytes():
+    b = _bench()
+    # state r+w 2*(51*12*4 + 7*4), action 8, obs 15*4*4, reward 4, flags 2, episode stats 8
+    assert b.algorithmic_bytes_per_env_step(51, 15, 4) == 5214
+    assert b.algorithmic_bytes_per_env_step(51, 30, 4) == 5214 + 4 * 15 * 4
+
+
+def test_minibatch_step_flops():
+    b = _bench()
+    S, H = 60, 256
+    W = S * H + 3 * H * H + 3 * H  # matrix parameters of ActorCritic
+    assert W == 212736
+    assert b.ppo_flops_per_sample(S, H) == 6 * W
+    assert b.ppo_flops_per_sample(S, H) * 4096 == 5228199936
+
+
+def test_cli_defaults(monkeypatch):
+    b = _bench()
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    a = b.parse()
+    assert (a.gpus, a.steps, a.warmup, a.envs, a.hidden, a.epochs, a.minibatches) == \
+        (1, 5, 2, 4096, 256, 8, 32)
