@@ -776,14 +776,17 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
             v.x < ROAD_LENGTH + LANE_VEH_LEN))
         continue;  // is_reachable_from
       if (hm_absf(v.spd) < 1.0f) continue;
+      // mobil's two tests are pure and both must hold: the cheap one (own acceleration gain,
+      // free-road term shared) first, so the follower's IDM (a pow) runs only for the few
+      // candidates that would gain; same decision as upstream's order
+      const float spa = idm_with_front(a_free, v.spd, v.x, ch, sh, fi[s] >= 0, np_x[q],
+                                       np_spd[q], np_c[q], np_s[q]);
+      if ((spa - self_a) < LANE_CHANGE_MIN_ACC_GAIN) continue;
       float nfp = 0.0f;
       if (ri[s] >= 0)
         nfp = idm_acc(nf_spd[q], nf_tsp[q], nf_x[q], nf_c[q], nf_s[q], true, v.x, v.spd, ch, sh,
                       v.dlt, limit);
       if (nfp < -LANE_CHANGE_MAX_BRAKING_IMPOSED) continue;
-      const float spa = idm_with_front(a_free, v.spd, v.x, ch, sh, fi[s] >= 0, np_x[q],
-                                       np_spd[q], np_c[q], np_s[q]);
-      if ((spa - self_a) < LANE_CHANGE_MIN_ACC_GAIN) continue;
       ntl = c;
     }
   }
