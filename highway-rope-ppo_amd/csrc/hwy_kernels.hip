@@ -735,22 +735,15 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   const int sop = fi[1] >= 0 ? fi[1] : lane;
   const float op_x = shf(v.x, sop), op_spd = shf(v.spd, sop), op_c = shf(ch, sop),
               op_s = shf(sh, sop);
-  float np_x[2], np_spd[2], np_c[2], np_s[2], nf_x[2], nf_spd[2], nf_c[2], nf_s[2], nf_tsp[2];
+  float np_x[2], np_spd[2], np_c[2], np_s[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int s = 2 * q;  // slot 0 (left, ln-1) and slot 2 (right, ln+1)
     const int a = fi[s] >= 0 ? fi[s] : lane;
-    const int b = ri[s] >= 0 ? ri[s] : lane;
     np_x[q] = shf(v.x, a);
     np_spd[q] = shf(v.spd, a);
     np_c[q] = shf(ch, a);
     np_s[q] = shf(sh, a);
-    nf_x[q] = shf(v.x, b);
-    nf_spd[q] = shf(v.spd, b);
-    nf_c[q] = shf(ch, b);
-    nf_s[q] = shf(sh, b);
-    const float tsp_b = shf(v.tsp, b);  // unconditional: ds_bpermute needs all lanes active
-    nf_tsp[q] = (b == 0) ? 0.0f : tsp_b;  // plain Vehicle (ego) has no target_speed
   }
 
   // acceleration(self, front on own lane): IDM term and MOBIL's self_a
@@ -763,9 +756,13 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   }
 
   // IDMVehicle.change_lane_policy -> mobil, side lanes left then right (POLITENESS = 0, so the
-  // followers' unchanged-lane terms multiply by zero and are not evaluated)
+  // followers' unchanged-lane terms multiply by zero and are not evaluated).  mobil's two tests
+  // are pure and both must hold, so the cheap one (own acceleration gain, free-road term shared)
+  // runs first, and the new followers' data and IDM (a pow) only for the candidates that would
+  // gain -- rarely any in a frame; the decision is upstream's.
   SEC(sp, 2);
   int ntl = v.tl;
+  bool gain[2] = {false, false};
   if (fire) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -776,18 +773,32 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
             v.x < ROAD_LENGTH + LANE_VEH_LEN))
         continue;  // is_reachable_from
       if (hm_absf(v.spd) < 1.0f) continue;
-      // mobil's two tests are pure and both must hold: the cheap one (own acceleration gain,
-      // free-road term shared) first, so the follower's IDM (a pow) runs only for the few
-      // candidates that would gain; same decision as upstream's order
       const float spa = idm_with_front(a_free, v.spd, v.x, ch, sh, fi[s] >= 0, np_x[q],
                                        np_spd[q], np_c[q], np_s[q]);
-      if ((spa - self_a) < LANE_CHANGE_MIN_ACC_GAIN) continue;
+      gain[q] = !((spa - self_a) < LANE_CHANGE_MIN_ACC_GAIN);
+    }
+  }
+  if (wave_any(gain[0] || gain[1])) {
+    float nf_x[2], nf_spd[2], nf_c[2], nf_s[2], nf_tsp[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {  // all lanes active: ds_bpermute
+      const int b = ri[2 * q] >= 0 ? ri[2 * q] : lane;
+      nf_x[q] = shf(v.x, b);
+      nf_spd[q] = shf(v.spd, b);
+      nf_c[q] = shf(ch, b);
+      nf_s[q] = shf(sh, b);
+      const float tsp_b = shf(v.tsp, b);
+      nf_tsp[q] = (b == 0) ? 0.0f : tsp_b;  // plain Vehicle (ego) has no target_speed
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {  // left, then right (the right one overrides)
+      if (!gain[q]) continue;
       float nfp = 0.0f;
-      if (ri[s] >= 0)
+      if (ri[2 * q] >= 0)
         nfp = idm_acc(nf_spd[q], nf_tsp[q], nf_x[q], nf_c[q], nf_s[q], true, v.x, v.spd, ch, sh,
                       v.dlt, limit);
       if (nfp < -LANE_CHANGE_MAX_BRAKING_IMPOSED) continue;
-      ntl = c;
+      ntl = v.ln - 1 + 2 * q;
     }
   }
 
