@@ -1050,20 +1050,16 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
     for (int rr = 0; rr < RPW; ++rr) {
       const int lr = RPW * w + rr;
       if (lr >= nrows) break;
-      const int b = row0 + lr;
       float* arow = AC + lr * PA;
       const float dmu0 = lane_f(c_dmu0, rr), dmu1 = lane_f(c_dmu1, rr), dv = lane_f(c_dv, rr);
-      float* grow = r.dac + (long)b * 2 * H;
 #pragma unroll
       for (int q = 0; q < QH; ++q) {
         const int col = lane + 64 * q;
         const float a = arow[col], cc = arow[H + col];
         const float da = a > 0.0f ? (dmu0 * wa0[q] + dmu1 * wa1[q]) : 0.0f;
         const float dc = cc > 0.0f ? dv * wc[q] : 0.0f;
-        arow[col] = da;
+        arow[col] = da;  // dac: the image is copied to HBM whole after the barrier
         arow[H + col] = dc;
-        grow[col] = da;
-        grow[H + col] = dc;
         ga0[q] += dmu0 * a;
         ga1[q] += dmu1 * a;
         gc[q] += dv * cc;
@@ -1085,6 +1081,7 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
     }
   }
   __syncthreads();
+  rows_out<NT>(AC, PA, r.dac + (long)row0 * 2 * H, 2 * H, 2 * H, nrows);
   PSEC(4);
   // dh2 = (dac [Wa1; Wc1]) * (h2 > 0)   ([Wa1; Wc1] is [2H][H]: k-major); the two halves of
   // K = 2H (Wa1 rows, Wc1 rows) are summed at the end
