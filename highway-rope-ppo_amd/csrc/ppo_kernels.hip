@@ -1,19 +1,21 @@
-// ppo_kernels.hip -- fused PPO minibatch step for gfx950 (include/hwy_ppo.h).
+// ppo_kernels.hip -- PPO minibatch step and batched acting for gfx950 (include/hwy_ppo.h).
 //
-// One minibatch step of the reference's PPOAgent.update (ppo/agent.py:216-252) as 11 launches:
-//   fwd:  h1 = relu(gather(states) W1^T + b1)            gemm64<A row-major+gather, B NT, bias+relu>
-//         h2 = relu(h1 W2^T + b2)
-//         ac = relu(h2 [Wa1;Wc1]^T + [ba1;bc1])          actor/critic first layers as one GEMM
-//   head: mean, value, log-prob, entropy, ratio, clipped surrogate, MSE, their gradients, the
-//         head weight/bias/log_std partials and the metrics, one row per thread-group pass
-//   bwd:  dh2 = (dac [Wa1;Wc1]) * (h2 > 0)               gemm64<.., B NN, relu mask>
-//         d[Wa1;Wc1] = dac^T h2, d[ba1;bc1] = colsum(dac)   split-K partial slabs
-//         dh1 = (dh2 W2) * (h1 > 0); dW2 = dh2^T h1; dW1 = dh1^T gather(states)
-//   reduce: partial slabs -> flat grads (fixed order, deterministic) + sum-of-squares partials
-//   opt:  clip_grad_norm_ + Adam (torch.optim.Adam formula) over the flat parameter buffer
-// GEMM core: 64x64 output tile per 256-thread workgroup, each wave a 32x32 tile accumulated
-// with v_mfma_f32_32x32x2_f32 (exact fp32 products), K staged 32 at a time through LDS with
-// the next tile prefetched into registers during the MFMAs.
+// One minibatch step of the reference's PPOAgent.update (ppo/agent.py:216-252).
+//
+// Fused path (S % 4 == 0, S <= 256, H a multiple of 64 up to 512): four launches, captured per
+// epoch in one HIP graph:
+//   ppo_rows   16 minibatch rows per workgroup: forward (h1, h2, [a1|c1]), the loss head
+//              (ratio, clipped surrogate, MSE, entropy, their gradients, head-parameter
+//              partials), backward data gradients (dh2, dh1); weights streamed from a tile image
+//   ppo_wgrad  dW = (output gradient)^T (input) as 128x64 tiles over 8 row slices (one per XCD)
+//              plus bias column sums, the head-parameter sums and the metrics row
+//   ppo_wsum   the 8 slice partials summed in slice order, sum-of-squares partials
+//   ppo_adam   clip_grad_norm_ + Adam (torch.optim.Adam formula), the tile image rewritten
+// ppo_act is ppo_rows' forward + a sampling head (ActorCritic.act on a batch).
+//
+// General path (other shapes): 11 launches of a 64x64-tile GEMM (gemm64 / gemm64v), the loss
+// head kernel (ppo_head), split-K partial slabs and one deterministic reduction (ppo_reduce).
+// All GEMMs use v_mfma_f32_*_f32: exact fp32 products, fp32 accumulation.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
