@@ -13,7 +13,8 @@
  *   actor_mean.2.{weight,bias} log_std critic.0.{weight,bias} critic.2.{weight,bias}
  * (weights [out, in] row-major, as nn.Linear stores them).
  *
- * All math is fp32; GEMMs use v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulate).
+ * All math is fp32; GEMMs use v_mfma_f32_16x16x4_f32 / v_mfma_f32_32x32x2_f32 (exact fp32
+ * products, fp32 accumulate).
  * Calls are asynchronous, allocate nothing and are hipGraph-capturable.
  *
  * Weight tile image: on the fused path (S % 4 == 0, S <= 256, H <= 512) the row kernel streams
