@@ -4,6 +4,14 @@ Same launch sequence and status dict: acquire device -> seed -> logger -> make_e
 ``env.to(device)`` when the wrapper has it -> state/action dims -> PPOAgent ->
 train_with_experiment_name -> {"status": "COMPLETED"|"FAILED", ...}.  Experiment.extra may carry
 ``num_envs`` (lockstep envs, > 1 selects the vectorised loop) and ``num_minibatches``.
+
+Launched under torchrun (WORLD_SIZE > 1) one experiment spans the ranks, one GPU each: the
+runner joins the process group (RCCL, or ``HWY_DIST_BACKEND``), gives rank r the envs
+r*num_envs.. of world*num_envs on the shared seed schedule and hands the group to PPOAgent
+(weights broadcast from rank 0, gradients and advantage statistics all-reduced).  Rank 0 logs,
+evaluates and writes the artifacts; the other ranks' results carry ``rank``.  The reference
+instead runs one single-GPU process per experiment and oversubscribes the GPUs
+(SURVEY.md §8(f)).
 """
 
 from __future__ import annotations
@@ -33,7 +41,8 @@ class DevicePool:
         import os
 
         if device is None and torch.cuda.is_available():
-            device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", 0)))
+            device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", 0))
+                                  % max(1, torch.cuda.device_count()))
         self.device = torch.device(device) if device is not None else torch.device("cpu")
 
     def acquire(self):
@@ -51,13 +60,33 @@ class ExperimentRunner:
         self.base_config = base_env_config
         self.pool = device_pool or DevicePool()
 
-    def _create_agent(self, state_dim, action_dim, hp, logger, device, extra=None):
+    @staticmethod
+    def _process_group(device):
+        """The torchrun world as a process group, or None for a single-process launch."""
+        import os
+
+        import torch.distributed as dist
+
+        if int(os.environ.get("WORLD_SIZE", "1")) <= 1 and not dist.is_initialized():
+            return None
+        if not dist.is_initialized():
+            backend = os.environ.get("HWY_DIST_BACKEND") or (
+                "nccl" if device.type == "cuda" else "gloo")
+            if backend == "nccl":
+                torch.cuda.set_device(device)
+                dist.init_process_group("nccl", device_id=device)
+            else:
+                dist.init_process_group(backend)
+        return dist.group.WORLD if dist.get_world_size() > 1 else None
+
+    def _create_agent(self, state_dim, action_dim, hp, logger, device, extra=None,
+                      process_group=None):
         extra = extra or {}
         return PPOAgent(state_dim=state_dim, action_dim=action_dim, lr=hp.lr, gamma=hp.gamma,
                         lam=hp.lam, eps_clip=hp.clip_eps, value_coef=hp.value_coef,
                         entropy_coef=hp.entropy_coef, max_grad_norm=hp.max_grad_norm,
                         epochs=hp.epochs, batch_size=hp.batch_size, hidden_dim=hp.hidden_dim,
-                        logger=logger, device=device,
+                        logger=logger, device=device, process_group=process_group,
                         num_minibatches=extra.get("num_minibatches"))
 
     def launch(self, exp: Experiment) -> Dict[str, Any]:
@@ -66,8 +95,18 @@ class ExperimentRunner:
         logger = None
         try:
             with self.pool.acquire() as device:
+                group = self._process_group(device)
+                rank, world = ((torch.distributed.get_rank(group),
+                                torch.distributed.get_world_size(group))
+                               if group is not None else (0, 1))
                 set_random_seeds(exp.seed)
-                logger = setup_experiment_logger(exp.name)
+                if rank == 0:
+                    logger = setup_experiment_logger(exp.name)
+                else:
+                    results["rank"] = rank
+                    logger = logging.getLogger(f"hwy.{exp.name}.rank{rank}")
+                    logger.addHandler(logging.NullHandler())
+                    logger.propagate = False
                 logger.info(f"[{exp.name}] Acquired device: {device} | Seed: {exp.seed}")
                 logger.info(f"[{exp.name}] Condition: {exp.condition.name} | HPs: {exp.hp}")
                 env = None
@@ -77,6 +116,11 @@ class ExperimentRunner:
                         overrides.setdefault("num_envs", exp.extra["num_envs"])
                     if device.type == "cuda":
                         overrides.setdefault("device", device)
+                    if group is not None:
+                        e = int(overrides.get("num_envs", 1))
+                        if e <= 1:
+                            raise ValueError("a multi-rank experiment needs extra['num_envs'] > 1")
+                        overrides.update(env_offset=rank * e, global_envs=world * e)
                     env = make_env(exp.condition, self.base_config, d_embed=exp.hp.d_embed,
                                    env_overrides=overrides)
                     if hasattr(env, "to") and callable(env.to):
@@ -86,7 +130,8 @@ class ExperimentRunner:
                     state_dim = int(np.prod(env.observation_space.shape))
                     action_dim = env.action_space.shape[0]
                     logger.info(f"[{exp.name}] state_dim={state_dim}, action_dim={action_dim}")
-                    agent = self._create_agent(state_dim, action_dim, exp.hp, logger, device, exp.extra)
+                    agent = self._create_agent(state_dim, action_dim, exp.hp, logger, device,
+                                               exp.extra, process_group=group)
                     rewards, avg_rewards, metrics = train_with_experiment_name(
                         env=env, agent=agent, max_episodes=exp.max_episodes,
                         target_reward=exp.target_reward,

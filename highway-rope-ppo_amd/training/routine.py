@@ -212,12 +212,18 @@ def train_with_experiment_name(env, agent, max_episodes=500, target_reward=0.0, 
     os.makedirs(checkpoint_dir, exist_ok=True)
     tracker = _EvalTracker(env, agent, exp_seed, target_reward, checkpoint_dir, experiment_name,
                            metrics_history, logger, exp_prefix, start_time)
-    logger.info(f"{exp_prefix} Performing initial evaluation...")
-    tracker.initial()
+    rank, _ = _rank_world(getattr(agent, "_dist", None))
+    if rank == 0:
+        logger.info(f"{exp_prefix} Performing initial evaluation...")
+        tracker.initial()
+    if not _is_vector(env) and getattr(agent, "_dist", None) is not None:
+        raise ValueError("a process group needs the vectorised env (num_envs > 1)")
     loop = _train_vector if _is_vector(env) else _train_single
     episode_rewards, training_episodes, total_steps = loop(
         env, agent, max_episodes, log_interval, eval_interval, steps_per_update, exp_seed, logger,
         exp_prefix, metrics_history, tracker, start_time)
+    if rank != 0:
+        return tracker.rewards, tracker.avg_rewards, metrics_history
     _save_artifacts(artifacts_dir, checkpoint_dir, experiment_name, metrics_history,
                     training_episodes, episode_rewards, tracker.eval_episodes, tracker.rewards,
                     tracker.avg_rewards, target_reward, total_steps, logger, exp_prefix)
@@ -277,9 +283,16 @@ def _train_single(env, agent, max_episodes, log_interval, eval_interval, steps_p
 
 def _train_vector(env, agent, max_episodes, log_interval, eval_interval, steps_per_update,
                   exp_seed, logger, prefix, mh, tracker, start_time):
-    """E lockstep envs, device rollout of T steps, batched PPO update."""
+    """E lockstep envs, device rollout of T steps, batched PPO update.
+
+    With a process group on the agent (one rank per GPU, envs env_offset = rank*E of world*E),
+    every rank steps its own E envs and joins the update's collectives; the episode stream is
+    gathered so all ranks count the same episodes and stop after the same update, and rank 0
+    alone evaluates and writes artifacts."""
     from ppo.agent import RolloutBuffer
 
+    group = getattr(agent, "_dist", None)
+    rank, world = _rank_world(group)
     base = env.unwrapped
     E = base.num_envs
     sd = _flat_dim(env)
@@ -299,27 +312,48 @@ def _train_vector(env, agent, max_episodes, log_interval, eval_interval, steps_p
                            buf.rewards[t], buf.terminated[t], buf.truncated[t],
                            buf.ep_return[t], buf.ep_length[t])
             torch.bitwise_or(buf.terminated[t], buf.truncated[t], out=buf.dones[t])
-        total_steps += T * E
+        total_steps += T * E * world
         with torch.no_grad():
             _, _, last_v = agent.actor_critic.forward(buf.states[T])
         upd = agent.update_rollout(buf, last_v.squeeze(-1))
-        # episode bookkeeping, in (step, env) order
-        dones = buf.dones.cpu().numpy().astype(bool)
-        rets = buf.ep_return.cpu().numpy()
-        for t, e in zip(*np.nonzero(dones)):
+        # episode bookkeeping, in (step, global env) order -- identical on every rank
+        for r in _episode_ends(buf.dones, buf.ep_return, group):
             if episode_num >= max_episodes:
                 break
             episode_num += 1
-            r = float(rets[t, e])
+            r = float(r)
             episode_rewards.append(r)
             training_episodes.append(episode_num)
             mh["episode_rewards"].append(r)
             mh["episode_numbers"].append(episode_num)
             _log_episode(logger, prefix, episode_num, r, episode_rewards, log_interval,
                          total_steps, start_time)
-            if episode_num % eval_interval == 0:
+            if episode_num % eval_interval == 0 and rank == 0:
                 tracker.on_episode(episode_num)
-        mh["policy_updates"].append({"episode": episode_num, "steps": T * E,
+        mh["policy_updates"].append({"episode": episode_num, "steps": T * E * world,
                                      "time": time.time() - t_update, **upd})
         buf.states[0].copy_(buf.states[T])
     return episode_rewards, training_episodes, total_steps
+
+
+def _rank_world(group):
+    if group is None:
+        return 0, 1
+    return torch.distributed.get_rank(group), torch.distributed.get_world_size(group)
+
+
+def _episode_ends(dones, rets, group=None):
+    """Returns of the episodes that ended in a [T, E] rollout, in (step, env) order.
+
+    Over a process group each rank's [T, E] slice is all-gathered and laid side by side, so
+    every rank sees the [T, world*E] stream one process stepping all world*E envs (rank r's at
+    r*E..) would, and counts the same episodes in the same order."""
+    pack = torch.stack([dones.to(torch.float64), rets.to(torch.float64)])
+    if group is not None:
+        if torch.distributed.get_backend(group) == "gloo":
+            pack = pack.cpu()
+        parts = [torch.empty_like(pack) for _ in range(torch.distributed.get_world_size(group))]
+        torch.distributed.all_gather(parts, pack.contiguous(), group=group)
+        pack = torch.cat(parts, dim=2)
+    pack = pack.cpu().numpy()
+    return pack[1][pack[0] != 0]

@@ -90,3 +90,49 @@ def test_sharded_update_equals_single_process(tmp_path):
     agent._run_epochs(cat["s"], cat["z"], cat["lp"], adv_n, cat["r"], batches)
     for k, v in agent.actor_critic.state_dict().items():
         torch.testing.assert_close(r0["state"][k], v, rtol=2e-5, atol=2e-6, msg=k)
+
+
+# ---- the runner's episode stream over ranks (training/routine.py _episode_ends) ----
+T_EP, E_EP = 5, 6
+
+
+def _episode_slice(rank):
+    g = np.random.default_rng(300 + rank)
+    dones = torch.as_tensor(g.random((T_EP, E_EP)) < 0.3)
+    rets = torch.as_tensor(g.normal(size=(T_EP, E_EP)).astype(np.float32) * 10)
+    return dones, rets
+
+
+def _episode_worker(rank, world, port, out_dir):
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.join(os.path.dirname(here), "highway-rope-ppo_amd"), here]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    from training.routine import _episode_ends
+
+    ends = _episode_ends(*_episode_slice(rank), torch.distributed.group.WORLD)
+    np.save(os.path.join(out_dir, f"ends{rank}.npy"), ends)
+    torch.distributed.destroy_process_group()
+
+
+def test_episode_ends_single_process_order():
+    from training.routine import _episode_ends
+
+    dones, rets = _episode_slice(0)
+    want = [float(rets[t, e]) for t in range(T_EP) for e in range(E_EP) if dones[t, e]]
+    np.testing.assert_array_equal(_episode_ends(dones, rets), np.array(want))
+
+
+def test_episode_ends_gathered_over_ranks_in_global_env_order(tmp_path):
+    """Every rank counts the episodes of one process stepping both ranks' envs side by side
+    (rank r's envs at r*E..), so all ranks stop after the same update."""
+    port = _free_port()
+    mp.start_processes(_episode_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    (d0, r0), (d1, r1) = _episode_slice(0), _episode_slice(1)
+    dones, rets = torch.cat([d0, d1], 1), torch.cat([r0, r1], 1)
+    want = [float(rets[t, e]) for t in range(T_EP) for e in range(2 * E_EP) if dones[t, e]]
+    for r in range(2):
+        np.testing.assert_array_equal(np.load(tmp_path / f"ends{r}.npy"), np.array(want))

@@ -13,6 +13,8 @@ seed 42 136.8270, 1042 127.8022, 2042 132.6172; mean 132.42).
 Usage (GPU box):  python tools/train_parity.py --seeds 42 --out gpurun_out/train
     --num-envs 1   the reference's own loop (1 env, batch-1 select_action, 2048-step updates)
     --num-envs E   the lockstep loop (E envs, same hyperparameters, same episode budget)
+Under torchrun (--nproc-per-node N) each experiment spans the N GPUs with E envs per rank
+(experiments/runner.py); rank 0 prints and writes the summary.
 """
 
 from __future__ import annotations
@@ -94,6 +96,9 @@ def main():
                            delta=round(float(avg[-1]) - ref, 4))
         else:
             row["error"] = res.get("error_message")
+        if res.get("rank", 0) != 0:
+            continue
+        row["world_size"] = int(os.environ.get("WORLD_SIZE", "1"))
         results.append(row)
         print(json.dumps(row), flush=True)
         with open(os.path.join(out, "summary.jsonl"), "a") as f:
