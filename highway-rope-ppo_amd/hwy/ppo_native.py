@@ -125,20 +125,26 @@ def act_supported(S: int, H: int, A: int) -> bool:
 
 
 def fused_act(agent, states: torch.Tensor, deterministic: bool = False,
-              generator: Optional[torch.Generator] = None, out=None):
+              generator: Optional[torch.Generator] = None, out=None,
+              noise: Optional[torch.Tensor] = None):
     """ActorCritic.act (ppo/agent.py:86-95) through hwy_ppo_act: one launch for the forward,
     the Normal sample (noise drawn from `generator` exactly as act() draws it), tanh and the
     squashed log-prob.  Returns (action, pre_tanh, log_prob, value); `out` = four contiguous
     float32 device tensors of shapes (B, 2), (B, 2), (B,), (B,) to write them into instead
-    (e.g. the rollout buffer rows of this step)."""
+    (e.g. the rollout buffer rows of this step); `noise` = a pre-drawn contiguous float32
+    (B, 2) standard normal sample to use instead of drawing one."""
     flat = flat_params(agent)[0]
     B, S = states.shape
     H = agent.actor_critic.shared[0].weight.shape[0]
     dev = states.device
     states = states.contiguous()
-    noise = None
-    if not deterministic:
+    if deterministic:
+        noise = None
+    elif noise is None:
         noise = torch.randn((B, 2), device=dev, dtype=states.dtype, generator=generator)
+    elif (tuple(noise.shape) != (B, 2) or noise.dtype != torch.float32 or noise.device != dev
+          or not noise.is_contiguous()):
+        raise ValueError(f"fused_act noise must be contiguous float32 {(B, 2)} on {dev}")
     if out is None:
         action = torch.empty(B, 2, device=dev)
         pre = torch.empty(B, 2, device=dev)

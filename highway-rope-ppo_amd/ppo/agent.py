@@ -82,14 +82,17 @@ class ActorCritic(nn.Module):
 
     @torch.no_grad()
     def act(self, states: torch.Tensor, deterministic: bool = False,
-            generator: Optional[torch.Generator] = None):
-        """Batched device sampling: returns (action, pre_tanh, log_prob, value) tensors."""
+            generator: Optional[torch.Generator] = None, noise: Optional[torch.Tensor] = None):
+        """Batched device sampling: returns (action, pre_tanh, log_prob, value) tensors.
+        ``noise`` (same shape as the mean) is a pre-drawn standard normal sample to use instead
+        of drawing one from ``generator``."""
         mean, std, value = self.forward(states)
         if deterministic:
             z = mean
             logp = torch.zeros(mean.shape[0], device=mean.device)
         else:
-            eps = torch.randn(mean.shape, device=mean.device, dtype=mean.dtype, generator=generator)
+            eps = noise if noise is not None else torch.randn(
+                mean.shape, device=mean.device, dtype=mean.dtype, generator=generator)
             z = mean + std * eps
             logp = self.squashed_log_prob(Normal(mean, std, validate_args=False), z)
         return torch.tanh(z), z, logp, value.squeeze(-1)
@@ -176,10 +179,21 @@ class RolloutBuffer:
         self.dones = torch.zeros(T, E, device=device, dtype=torch.uint8)
         self.ep_return = torch.zeros(T, E, **kw)
         self.ep_length = torch.zeros(T, E, device=device, dtype=torch.int32)
+        self.noise = torch.zeros(T, E, action_dim, **kw)  # the rollout's sampling noise
 
     @property
     def n(self) -> int:
         return self.T * self.E
+
+    def draw_noise(self, generator: Optional[torch.Generator] = None) -> None:
+        """All T steps' standard normal sampling noise in one draw (one launch per rollout
+        instead of one per step); step t acts with ``noise[t]``."""
+        torch.randn(self.noise.shape, generator=generator, device=self.noise.device,
+                    out=self.noise)
+
+    def finish_dones(self) -> None:
+        """dones = terminated | truncated for the whole rollout, once."""
+        torch.bitwise_or(self.terminated, self.truncated, out=self.dones)
 
 
 class _Learner:
@@ -339,21 +353,33 @@ class PPOAgent:
             self.generator.manual_seed(int(seed) if seed is not None else torch.initial_seed() % (2**63))
 
     # ------------------------------------------------------------------ acting
-    def select_action(self, state, deterministic: bool = False, out=None):
+    def select_action(self, state, deterministic: bool = False, out=None, noise=None):
         """Batched (2-D tensor) or single-state acting.  For a batch, `out` may name the four
-        tensors (action, pre_tanh, log_prob, value) to write, e.g. a rollout buffer's rows."""
+        tensors (action, pre_tanh, log_prob, value) to write, e.g. a rollout buffer's rows, and
+        `noise` a pre-drawn (B, action_dim) standard normal sample (RolloutBuffer.draw_noise)."""
         if isinstance(state, torch.Tensor) and state.dim() == 2:
             if self._act_fused_ok(state):
                 from hwy.ppo_native import fused_act
 
-                return fused_act(self, state, deterministic, self.generator, out=out)
-            res = self.actor_critic.act(state, deterministic, generator=self.generator)
+                return fused_act(self, state, deterministic, self.generator, out=out, noise=noise)
+            res = self.actor_critic.act(state, deterministic, generator=self.generator,
+                                        noise=noise)
             if out is None:
                 return res
             for dst, src in zip(out, res):
                 dst.copy_(src.reshape(dst.shape))
             return tuple(out)
         return self.actor_critic.get_action(state, deterministic)
+
+    def value(self, states: torch.Tensor) -> torch.Tensor:
+        """V(s) for a batch, e.g. a rollout's bootstrap row: the value output of the fused act
+        launch when acting is fused, else the torch forward."""
+        if self._act_fused_ok(states):
+            from hwy.ppo_native import fused_act
+
+            return fused_act(self, states.contiguous(), True)[3]
+        with torch.no_grad():
+            return self.actor_critic.forward(states)[2].squeeze(-1)
 
     def _act_fused_ok(self, state: torch.Tensor) -> bool:
         """Batched acting runs through hwy_ppo_act (one launch) unless backend='torch'."""

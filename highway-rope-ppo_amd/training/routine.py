@@ -305,17 +305,17 @@ def _train_vector(env, agent, max_episodes, log_interval, eval_interval, steps_p
     total_steps = episode_num = 0
     while episode_num < max_episodes:
         t_update = time.time()
+        buf.draw_noise(agent.generator)
         for t in range(T):
             agent.select_action(buf.states[t], out=(buf.actions[t], buf.pre_tanh[t],
-                                                    buf.log_probs[t], buf.values[t]))
+                                                    buf.log_probs[t], buf.values[t]),
+                                noise=buf.noise[t])
             base.step_into(buf.actions[t], buf.states[t + 1].view(E, *base.obs_buf.shape[1:]),
                            buf.rewards[t], buf.terminated[t], buf.truncated[t],
                            buf.ep_return[t], buf.ep_length[t])
-            torch.bitwise_or(buf.terminated[t], buf.truncated[t], out=buf.dones[t])
+        buf.finish_dones()
         total_steps += T * E * world
-        with torch.no_grad():
-            _, _, last_v = agent.actor_critic.forward(buf.states[T])
-        upd = agent.update_rollout(buf, last_v.squeeze(-1))
+        upd = agent.update_rollout(buf, agent.value(buf.states[T]))
         # episode bookkeeping, in (step, global env) order -- identical on every rank
         for r in _episode_ends(buf.dones, buf.ep_return, group):
             if episode_num >= max_episodes:

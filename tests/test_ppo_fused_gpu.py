@@ -212,3 +212,32 @@ def test_fused_act_from_tile_image_equals_params_path(S, H):
         got = fused_act(b, x, deterministic=True)
     for r, g in zip(ref, got):
         torch.testing.assert_close(g, r, rtol=1e-4, atol=2e-5)
+
+
+def test_rollout_noise_value_and_dones_helpers():
+    """Pre-drawn rollout noise (RolloutBuffer.draw_noise, one draw per rollout) gives the same
+    sample through the kernel and ActorCritic.act; agent.value is the critic's V(s);
+    finish_dones = terminated | truncated."""
+    from ppo.agent import RolloutBuffer
+
+    S, H, T, E = 60, 256, 3, 300
+    a, b = _agents(S, H)
+    buf = RolloutBuffer(T, E, S, 2, DEV)
+    g = torch.Generator(device=DEV).manual_seed(11)
+    buf.draw_noise(g)
+    g2 = torch.Generator(device=DEV).manual_seed(11)
+    assert torch.equal(buf.noise, torch.randn(T, E, 2, generator=g2, device=DEV))
+    s = torch.randn(E, S, device=DEV)
+    with torch.no_grad():
+        ref = a.actor_critic.act(s, noise=buf.noise[1])
+        got = b.select_action(s, noise=buf.noise[1])
+        for r, x in zip(ref, got):
+            torch.testing.assert_close(x, r, rtol=1e-4, atol=2e-5)
+        torch.testing.assert_close(b.value(s), a.actor_critic.forward(s)[2].squeeze(-1),
+                                   rtol=1e-4, atol=2e-5)
+    with pytest.raises(ValueError):
+        b.select_action(s, noise=buf.noise[1][:, :1])
+    buf.terminated.copy_(torch.randint(0, 2, (T, E), device=DEV, dtype=torch.uint8))
+    buf.truncated.copy_(torch.randint(0, 2, (T, E), device=DEV, dtype=torch.uint8))
+    buf.finish_dones()
+    assert torch.equal(buf.dones, buf.terminated | buf.truncated)
