@@ -61,6 +61,52 @@ __device__ __forceinline__ float shf(float v, int src) {
   return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
 }
 __device__ __forceinline__ int shi(int v, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
+// DPP forms (VALU-local, no LDS round trip); all 64 lanes active.  GFX9 DPP controls:
+// wave_shr:1 0x138, row_shr:k 0x110+k, row_bcast:15 0x142, row_bcast:31 0x143,
+// quad_perm 0x00-0xFF, row_mirror 0x140, row_half_mirror 0x141.
+// lane i <- lane i-1; lane 0 keeps its own value
+__device__ __forceinline__ float shr1f(float v) {
+  const int b = __float_as_int(v);
+  return __int_as_float(__builtin_amdgcn_update_dpp(b, b, 0x138, 0xf, 0xf, false));
+}
+// lane i <- lane i+1; lane 63 keeps its own value
+__device__ __forceinline__ int shl1i(int v) {
+  return __builtin_amdgcn_update_dpp(v, v, 0x130, 0xf, 0xf, false);
+}
+__device__ __forceinline__ int shr1i(int v) {
+  return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xf, 0xf, false);
+}
+// lane i <- lane i^1
+__device__ __forceinline__ int swp1i(int v) {
+  return __builtin_amdgcn_update_dpp(v, v, 0xb1, 0xf, 0xf, false);
+}
+// inclusive prefix sum over the 64 lanes
+__device__ __forceinline__ int wave_incl_scan(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+  return x;
+}
+// max over the 64 lanes (exact: no NaN reaches it), uniform result
+__device__ __forceinline__ float wave_max_f(float v) {
+  int b = __float_as_int(v);
+  b = __float_as_int(hm_maxf(__int_as_float(b), __int_as_float(
+      __builtin_amdgcn_update_dpp(b, b, 0xb1, 0xf, 0xf, false))));
+  b = __float_as_int(hm_maxf(__int_as_float(b), __int_as_float(
+      __builtin_amdgcn_update_dpp(b, b, 0x4e, 0xf, 0xf, false))));
+  b = __float_as_int(hm_maxf(__int_as_float(b), __int_as_float(
+      __builtin_amdgcn_update_dpp(b, b, 0x141, 0xf, 0xf, false))));
+  b = __float_as_int(hm_maxf(__int_as_float(b), __int_as_float(
+      __builtin_amdgcn_update_dpp(b, b, 0x140, 0xf, 0xf, false))));
+  b = __float_as_int(hm_maxf(__int_as_float(b), __int_as_float(
+      __builtin_amdgcn_update_dpp(b, b, 0x142, 0xa, 0xf, false))));
+  b = __float_as_int(hm_maxf(__int_as_float(b), __int_as_float(
+      __builtin_amdgcn_update_dpp(b, b, 0x143, 0xc, 0xf, false))));
+  return __int_as_float(__builtin_amdgcn_readlane(b, 63));
+}
 __device__ __forceinline__ uint64_t ballot(bool p) { return (uint64_t)__ballot(p); }
 __device__ __forceinline__ bool wave_any(bool p) { return ballot(p) != 0ull; }
 __device__ __forceinline__ void wave_lds_sync() {
@@ -571,6 +617,19 @@ __device__ __forceinline__ uint64_t shf64(uint64_t v, int src) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+__device__ __forceinline__ uint64_t shl1_64(uint64_t v) {
+  return ((uint64_t)(uint32_t)shl1i((int)(uint32_t)(v >> 32)) << 32) |
+         (uint32_t)shl1i((int)(uint32_t)v);
+}
+__device__ __forceinline__ uint64_t shr1_64(uint64_t v) {
+  return ((uint64_t)(uint32_t)shr1i((int)(uint32_t)(v >> 32)) << 32) |
+         (uint32_t)shr1i((int)(uint32_t)v);
+}
+__device__ __forceinline__ uint64_t swp1_64(uint64_t v) {
+  return ((uint64_t)(uint32_t)swp1i((int)(uint32_t)(v >> 32)) << 32) |
+         (uint32_t)swp1i((int)(uint32_t)v);
+}
+
 // order-preserving u32 image of x (+0 and -0 map together); absent -> above every float
 __device__ __forceinline__ uint64_t road_key(float x, bool present, int lane) {
   const uint32_t u = hm_f2bits(x + 0.0f);
@@ -582,14 +641,14 @@ __device__ __forceinline__ uint64_t road_key(float x, bool present, int lane) {
 // Re-validates (or rebuilds) the order for the current positions.
 __device__ void road_order(int lane, const Veh& v, uint64_t pres, RoadOrder& o) {
   const uint64_t key = road_key(v.x, v.present, lane);
-  const int nxt = lane < WAVE - 1 ? lane + 1 : lane;
   bool sorted = false;
   if (o.valid) {
     uint64_t kp = shf64(key, o.ord);
-    uint64_t kn = shf64(kp, nxt);
+    uint64_t kn = shl1_64(kp);  // the next position's key (DPP)
     sorted = !wave_any(lane < WAVE - 1 && !(kp < kn));
     // a few overtakes since the last frame: odd-even transposition rounds on (key, vehicle)
-    // in position space usually restore the order without a full re-rank
+    // in position space usually restore the order without a full re-rank; the partner is
+    // lane ^ 1 in the even phase and lane + 1 / lane - 1 (odd / even lane) in the odd one
     int ordp = o.ord;
     for (int round = 0; round < 3 && !sorted; ++round) {
 #pragma unroll
@@ -597,13 +656,22 @@ __device__ void road_order(int lane, const Veh& v, uint64_t pres, RoadOrder& o) 
         const bool left = (lane & 1) == ph;
         int partner = left ? lane + 1 : lane - 1;
         if (partner < 0 || partner >= WAVE) partner = lane;
-        const uint64_t pk = shf64(kp, partner);
-        const int po = shi(ordp, partner);
+        uint64_t pk;
+        int po;
+        if (ph == 0) {
+          pk = swp1_64(kp);
+          po = swp1i(ordp);
+        } else {
+          const uint64_t up = shl1_64(kp), dn = shr1_64(kp);
+          const int uo = shl1i(ordp), dno = shr1i(ordp);
+          pk = left ? up : dn;
+          po = left ? uo : dno;
+        }
         const bool swap = partner != lane && (left ? (pk < kp) : (kp < pk));
         kp = swap ? pk : kp;
         ordp = swap ? po : ordp;
       }
-      kn = shf64(kp, nxt);
+      kn = shl1_64(kp);
       sorted = !wave_any(lane < WAVE - 1 && !(kp < kn));
     }
     if (sorted) {
@@ -651,7 +719,7 @@ __device__ __forceinline__ LaneScan lane_scan(int lane, const Veh& v, uint64_t p
   const float xp = shf(v.x, o.ord);
   L.yp = shf(v.y, o.ord);
   L.okp = lane < npres && -LANE_VEH_LEN <= xp && xp < ROAD_LENGTH + LANE_VEH_LEN;
-  const float xprev = shf(xp, lane > 0 ? lane - 1 : 0);
+  const float xprev = shr1f(xp);
   const uint64_t starts = ballot(lane == 0 || !(xprev == xp));  // x-group starts (bit 0 set)
   const int g = 63 - __builtin_clzll(starts & ((2ull << o.rk) - 1ull));  // rk = 63: all ones
   const bool selfok = v.x == v.x;
@@ -897,8 +965,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   float vabs = v.present ? hm_absf(v.spd) : 0.0f;
   bool nonfinite = v.present && !(hm_absf(v.x) <= 3.0e38f && hm_absf(v.y) <= 3.0e38f &&
                                   hm_absf(v.spd) <= 3.0e38f);
-#pragma unroll
-  for (int m = 1; m < WAVE; m <<= 1) vabs = hm_maxf(vabs, shf(vabs, lane ^ m));
+  vabs = wave_max_f(vabs);
   const float xbound = wave_any(nonfinite) ? __builtin_huge_valf()
                                            : (VEH_DIAGONAL + vabs * dt) * 1.001f + 1.0e-3f;
   uint64_t pm = 0ull;
@@ -929,12 +996,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   // by (partner + 1) in the high word.
   uint64_t own = pm & (lane >= WAVE - 1 ? 0ull : (~0ull << (lane + 1)));
   const int cnt = __popcll(own);
-  int off = cnt;  // inclusive scan of cnt over lanes
-#pragma unroll
-  for (int d = 1; d < WAVE; d <<= 1) {
-    const int t = shi(off, lane >= d ? lane - d : lane);
-    if (lane >= d) off += t;
-  }
+  int off = wave_incl_scan(cnt);
   const int total = rdli(off, WAVE - 1);
   off -= cnt;
   cl.imx[lane] = 0ull;
