@@ -768,10 +768,11 @@ __device__ __forceinline__ int front_on_lane(const hwy_config& C, int lane, cons
   return fa ? vf : -1;
 }
 
-// per-wave LDS of the collision pass (5.2 KB)
+// per-wave LDS of the collision pass (5.4 KB)
 struct CollLds {
   unsigned long long imx[WAVE], imy[WAVE];  // (partner + 1) << 32 | impact bits, max-reduced
   int crash[WAVE];
+  int pord[WAVE];                         // vehicle at each road-order position
   uint16_t plist[WAVE * (WAVE - 1) / 2];  // candidate pairs (a << 8 | b), a < b
 };
 
@@ -968,44 +969,44 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   vabs = wave_max_f(vabs);
   const float xbound = wave_any(nonfinite) ? __builtin_huge_valf()
                                            : (VEH_DIAGONAL + vabs * dt) * 1.001f + 1.0e-3f;
-  uint64_t pm = 0ull;
+  // x-sorted road order, in position space (lane = position p, holding vehicle ord[p]): the
+  // candidates are the pairs (p, p+o) whose |dx| is within the bound.  x is monotone along the
+  // order, so the run from p upwards is contiguous and every pair is found once, from its lower
+  // position; x at p+o comes from a one-lane DPP shift per step (equal x sit together; a NaN x,
+  // or any non-finite value, makes the bound infinite: every pair of present vehicles).
+  uint64_t om = 0ull;  // bit o: (p, p+o) is a candidate pair
   {
-    // x-sorted road order: the candidates of a vehicle are the run of positions around its
-    // own whose |dx| stays within the bound; walk both ways until every lane has left its run
-    // (equal x sit together; a NaN x, or any non-finite value, makes the bound infinite so
-    // the walk covers every present vehicle)
     const int npres = __popcll(pres);
     const float xs = shf(v.x, ro.ord);  // x at position `lane`
-    bool up = v.present, dn = v.present;
-    for (int o = 1; wave_any(up || dn); ++o) {
-      const int pu = ro.rk + o < WAVE ? ro.rk + o : WAVE - 1;
-      const int pd = ro.rk - o >= 0 ? ro.rk - o : 0;
-      const float xu = shf(xs, pu), xd = shf(xs, pd);
-      const int iu = shi(ro.ord, pu), id = shi(ro.ord, pd);
-      up = up && ro.rk + o < npres && !(hm_absf(xu - v.x) > xbound);
-      dn = dn && ro.rk - o >= 0 && !(hm_absf(xd - v.x) > xbound);
-      if (up) pm |= 1ull << iu;
-      if (dn) pm |= 1ull << id;
+    float xu = xs;
+    bool up = lane < npres;
+    for (int o = 1; wave_any(up); ++o) {
+      xu = __int_as_float(shl1i(__float_as_int(xu)));  // x at position lane + o
+      up = up && lane + o < npres && !(hm_absf(xu - xs) > xbound);
+      if (up) om |= 1ull << o;
     }
   }
   SEC(sp, 10);
-  // Each candidate pair {i < j} once, spread over the lanes: lane i lists its pairs at its
-  // exclusive prefix offset, then lane t takes pair t (64 per round).  Per vehicle, upstream
-  // keeps the impact of its highest-index partner (the last handle_collisions call that writes
-  // it) and ORs the crash flag; the translation therefore goes through a 64-bit LDS max keyed
-  // by (partner + 1) in the high word.
-  uint64_t own = pm & (lane >= WAVE - 1 ? 0ull : (~0ull << (lane + 1)));
-  const int cnt = __popcll(own);
+  // Each candidate pair once, spread over the lanes: position p lists its pairs (as vehicle
+  // indices a < b) at its exclusive prefix offset, then lane t takes pair t (64 per round).
+  // Per vehicle, upstream keeps the impact of its highest-index partner (the last
+  // handle_collisions call that writes it) and ORs the crash flag; the translation therefore
+  // goes through a 64-bit LDS max keyed by (partner + 1) in the high word.
+  const int cnt = __popcll(om);
   int off = wave_incl_scan(cnt);
   const int total = rdli(off, WAVE - 1);
   off -= cnt;
   cl.imx[lane] = 0ull;
   cl.imy[lane] = 0ull;
   cl.crash[lane] = 0;
-  while (own) {
-    const int j = __builtin_ctzll(own);
-    own &= own - 1ull;
-    cl.plist[off++] = (uint16_t)((lane << 8) | j);
+  cl.pord[lane] = ro.ord;
+  wave_lds_sync();
+  while (om) {
+    const int o = __builtin_ctzll(om);
+    om &= om - 1ull;
+    const int q = cl.pord[lane + o];
+    const int lo = ro.ord < q ? ro.ord : q, hi = ro.ord < q ? q : ro.ord;
+    cl.plist[off++] = (uint16_t)((lo << 8) | hi);
   }
   wave_lds_sync();
   for (int base = 0; base < total; base += WAVE) {
