@@ -1,0 +1,38 @@
+"""bench.py's N > 1 path as the driver launches it (torch.distributed.run, one process per
+rank), rehearsed with 2 ranks on one GPU: gloo stands in for RCCL (HWY_BENCH_DIST_BACKEND).
+Rank 0 prints one line; value is the whole job's env-steps over the max-over-ranks time."""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_bench_two_ranks_one_line():
+    env = dict(os.environ, HWY_BENCH_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--envs", "256", "--rollout", "8", "--minibatches", "4", "--epochs", "2"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["cpu_baseline"] is None
+    assert d["config"]["global_envs"] == 512 and d["roofline"]["includes_allreduce"] is True
+    assert abs(d["value"] - 512 * 8 * 2 / (d["ms_per_step"] * 2e-3)) / d["value"] < 0.01
