@@ -732,9 +732,11 @@ __device__ __forceinline__ uint64_t on_lane_mask(const LaneScan& L, int c) {
   return ballot(L.okp && hm_absf(lane_lat(L.yp, c)) <= LANE_WIDTH / 2.0f + 1.0f);
 }
 
+// Also returns qf[s], the road-order position of front s (this vehicle's own position when
+// there is none), for gathers from position-space copies one bpermute level earlier.
 __device__ __forceinline__ void neighbours_ordered(const hwy_config& C, int lane, const Veh& v,
                                                    uint64_t pres, const RoadOrder& o, int fi[3],
-                                                   int ri[3]) {
+                                                   int ri[3], int qfp[3]) {
   const LaneScan L = lane_scan(lane, v, pres, o);
   uint64_t m[3] = {0ull, 0ull, 0ull};
   for (int c = 0; c < C.lanes_count; ++c) {
@@ -751,6 +753,7 @@ __device__ __forceinline__ void neighbours_ordered(const hwy_config& C, int lane
     const int vf = shi(o.ord, qf), vr = shi(o.ord, qr);
     fi[s] = fa ? vf : -1;
     ri[s] = rb ? vr : -1;
+    qfp[s] = fa ? qf : o.rk;
   }
 }
 
@@ -797,22 +800,26 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   SEC(sp, 0);
   if (!ro.valid) road_order(lane, v, pres, ro);  // later frames: validated after the last move
   SEC(sp, 9);
-  neighbours_ordered(C, lane, v, pres, ro, fi, ri);
+  // position-space copies of the fronts' state (vehicle at position p on lane p), gathered
+  // alongside the order so the fronts' values are one bpermute from their positions
+  const float xq = shf(v.x, ro.ord), spdq = shf(v.spd, ro.ord), cq = shf(ch, ro.ord),
+              sq = shf(sh, ro.ord);
+  int qfp[3];
+  neighbours_ordered(C, lane, v, pres, ro, fi, ri, qfp);
   SEC(sp, 1);
 
-  // gathers (all lanes active)
-  const int sop = fi[1] >= 0 ? fi[1] : lane;
-  const float op_x = shf(v.x, sop), op_spd = shf(v.spd, sop), op_c = shf(ch, sop),
-              op_s = shf(sh, sop);
+  // gathers (all lanes active); a missing front reads this vehicle's own values (unused)
+  const int sop = qfp[1];
+  const float op_x = shf(xq, sop), op_spd = shf(spdq, sop), op_c = shf(cq, sop),
+              op_s = shf(sq, sop);
   float np_x[2], np_spd[2], np_c[2], np_s[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
-    const int s = 2 * q;  // slot 0 (left, ln-1) and slot 2 (right, ln+1)
-    const int a = fi[s] >= 0 ? fi[s] : lane;
-    np_x[q] = shf(v.x, a);
-    np_spd[q] = shf(v.spd, a);
-    np_c[q] = shf(ch, a);
-    np_s[q] = shf(sh, a);
+    const int a = qfp[2 * q];  // slot 0 (left, ln-1) and slot 2 (right, ln+1)
+    np_x[q] = shf(xq, a);
+    np_spd[q] = shf(spdq, a);
+    np_c[q] = shf(cq, a);
+    np_s[q] = shf(sq, a);
   }
 
   // acceleration(self, front on own lane): IDM term and MOBIL's self_a
