@@ -1262,8 +1262,7 @@ struct WgArgs {
 template <int NW = 4>
 __device__ __forceinline__ float block_sum4(float v, float* red) {
   const int t = threadIdx.x;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  v = wave_sum_dpp(v);
   __syncthreads();
   if ((t & 63) == 0) red[t >> 6] = v;
   __syncthreads();
@@ -1569,6 +1568,12 @@ __global__ void __launch_bounds__(256) ppo_wsum(WgArgs a) {
 #pragma unroll
   for (int zz = 0; zz < kMaxSplit; ++zz)
     if (zz < a.split) pv[zz] = *reinterpret_cast<const f32x4*>(sl + (long)zz * kWgPart + e);
+  // the bias partials of output row i0 + t load in the same round trip as the tile's
+  const bool bias_t = part == 0 && tj == 0 && t < kWgTM && i0 + t < M;
+  float bp[kMaxSplit];
+#pragma unroll
+  for (int zz = 0; zz < kMaxSplit; ++zz)
+    bp[zz] = (bias_t && zz < a.split) ? sl[(long)zz * kWgPart + kWgTM * kWgTN + t] : 0.0f;
   f32x4 v = pv[0];
 #pragma unroll
   for (int zz = 1; zz < kMaxSplit; ++zz)
@@ -1583,9 +1588,11 @@ __global__ void __launch_bounds__(256) ppo_wsum(WgArgs a) {
         sq += v[c4] * v[c4];
       }
   }
-  if (part == 0 && tj == 0 && t < kWgTM && i0 + t < M) {  // bias of output row i0 + t
+  if (bias_t) {  // bias of output row i0 + t
     float b = 0.0f;
-    for (int zz = 0; zz < a.split; ++zz) b += sl[(long)zz * kWgPart + kWgTM * kWgTN + t];
+#pragma unroll
+    for (int zz = 0; zz < kMaxSplit; ++zz)
+      if (zz < a.split) b += bp[zz];
     const int i = i0 + t;
     long bo;
     if (region == 0) bo = i < H ? a.off[P_BA1] + i : a.off[P_BC1] + (i - H);
@@ -1639,8 +1646,7 @@ __global__ void __launch_bounds__(kRedThreads) ppo_reduce(RedArgs r) {
     r.grads[i] = s;
     sq = s * s;
   }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) sq += __shfl_xor(sq, o);
+  sq = wave_sum_dpp(sq);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1763,8 +1769,7 @@ __global__ void __launch_bounds__(kRedThreads) ppo_sumsq(const float* g, int64_t
   __shared__ float red[kRedThreads / 64];
   const int64_t i = (int64_t)blockIdx.x * kRedThreads + threadIdx.x;
   float sq = i < n ? g[i] * g[i] : 0.0f;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) sq += __shfl_xor(sq, o);
+  sq = wave_sum_dpp(sq);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1784,14 +1789,9 @@ __global__ void __launch_bounds__(256) ppo_adam(OptArgs o) {
   const float g_raw = o.grads[ii], m_old = o.m[ii], v_old = o.v[ii], p_old = o.params[ii];
   float s = 0.0f;
   for (int k = threadIdx.x; k < o.nred; k += 256) s += o.norm_part[k];
-#pragma unroll
-  for (int q = 32; q >= 1; q >>= 1) s += __shfl_xor(s, q);
+  s = wave_sum_dpp(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const float total = sqrtf(((red[0] + red[1]) + red[2]) + red[3]);
-    const float c = o.max_norm / (total + 1e-6f);
-    coef_s = c < 1.0f ? c : 1.0f;
+  if (threadIdx.x == 64) {  // wave 1, while the norm partials combine
     // torch.optim.Adam (foreach, non-capturable): bias corrections in double on the host side
     // (beta ** t by binary powering: a few dependent multiplies instead of a double pow())
     const int t = o.counters[0];
@@ -1804,6 +1804,12 @@ __global__ void __launch_bounds__(256) ppo_adam(OptArgs o) {
     const double bc2 = 1.0 - p2;
     step_s = (float)((double)o.lr / bc1);
     bc2s_s = (float)sqrt(bc2);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float total = sqrtf(((red[0] + red[1]) + red[2]) + red[3]);
+    const float c = o.max_norm / (total + 1e-6f);
+    coef_s = c < 1.0f ? c : 1.0f;
   }
   __syncthreads();
   const float coef = coef_s;
