@@ -80,14 +80,14 @@ class ExperimentRunner:
         return dist.group.WORLD if dist.get_world_size() > 1 else None
 
     def _create_agent(self, state_dim, action_dim, hp, logger, device, extra=None,
-                      process_group=None):
+                      process_group=None, seed=None):
         extra = extra or {}
         return PPOAgent(state_dim=state_dim, action_dim=action_dim, lr=hp.lr, gamma=hp.gamma,
                         lam=hp.lam, eps_clip=hp.clip_eps, value_coef=hp.value_coef,
                         entropy_coef=hp.entropy_coef, max_grad_norm=hp.max_grad_norm,
                         epochs=hp.epochs, batch_size=hp.batch_size, hidden_dim=hp.hidden_dim,
                         logger=logger, device=device, process_group=process_group,
-                        num_minibatches=extra.get("num_minibatches"))
+                        num_minibatches=extra.get("num_minibatches"), seed=seed)
 
     def launch(self, exp: Experiment) -> Dict[str, Any]:
         results: Dict[str, Any] = {"experiment_name": exp.name, "status": "FAILED"}
@@ -130,8 +130,12 @@ class ExperimentRunner:
                     state_dim = int(np.prod(env.observation_space.shape))
                     action_dim = env.action_space.shape[0]
                     logger.info(f"[{exp.name}] state_dim={state_dim}, action_dim={action_dim}")
+                    # every rank seeds the global RNGs with exp.seed (the RankPE table and the
+                    # initial weights must agree), but each rank's sampling generator gets its
+                    # own stream, so global env r*E+e does not replay env e's exploration noise
+                    agent_seed = None if group is None else exp.seed * 1000003 + rank
                     agent = self._create_agent(state_dim, action_dim, exp.hp, logger, device,
-                                               exp.extra, process_group=group)
+                                               exp.extra, process_group=group, seed=agent_seed)
                     rewards, avg_rewards, metrics = train_with_experiment_name(
                         env=env, agent=agent, max_episodes=exp.max_episodes,
                         target_reward=exp.target_reward,

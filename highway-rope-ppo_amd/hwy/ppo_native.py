@@ -259,6 +259,13 @@ class FusedPPO:
         a.grads_modified = 1 if self.group is not None else 0
         return a
 
+    def _scalar_key(self):
+        ag = self.agent
+        g = ag.optimizer.param_groups[0]
+        return (float(ag.eps_clip), float(ag.value_coef), float(ag.entropy_coef),
+                float(ag.max_grad_norm), float(g["lr"]), tuple(map(float, g["betas"])),
+                float(g["eps"]))
+
     def _fwd_bwd(self, a):
         check(self.L.hwy_ppo_forward_backward(ctypes.byref(a), stream_ptr()), "hwy_ppo_forward_backward")
 
@@ -299,8 +306,10 @@ class FusedPPO:
     def run(self, states, pre_tanh, old_lp, adv, ret, perm: torch.Tensor) -> torch.Tensor:
         """All epochs of one update; returns the [epochs*nmb, 6] metrics rows (device)."""
         mb, nmb, epochs = self.mb, self.nmb, self.agent.epochs
+        # the captured graphs bake in the buffer addresses and the scalar hyper-parameters of
+        # PpoArgs: a change to either (an lr schedule, agent.eps_clip, ...) forces a recapture
         key = (states.data_ptr(), pre_tanh.data_ptr(), old_lp.data_ptr(), adv.data_ptr(),
-               ret.data_ptr(), perm.data_ptr())
+               ret.data_ptr(), perm.data_ptr()) + self._scalar_key()
         args = [self._args(states, pre_tanh, old_lp, adv, ret, perm.data_ptr() + i * mb * 8)
                 for i in range(nmb)]
         self.counters[1].zero_()

@@ -347,6 +347,7 @@ class PPOAgent:
         self.logger = logger or logging.getLogger(__name__)
         self.memory = PPOMemory(batch_size=batch_size, device=self.device)
         self._learner: Optional[_Learner] = None
+        self.updates = 0  # completed update() / update_rollout() calls (evaluation memo key)
         self.generator = None
         if self.device.type == "cuda":
             self.generator = torch.Generator(device=self.device)
@@ -472,6 +473,7 @@ class PPOAgent:
         out = self._finish_metrics(rows.cpu().numpy(), [int(b.numel()) for b in batches], values,
                                    returns)
         self.memory.clear()
+        self.updates += 1
         return out
 
     # ------------------------------------------------------------------ batched update
@@ -501,11 +503,11 @@ class PPOAgent:
         old_lp = buf.log_probs.reshape(n)
         ret = ret.reshape(n)
         adv = self.normalize_advantages(adv.reshape(n))
-        nmb = self.num_minibatches or max(1, n // self.batch_size)
         if perm is None:
             perm = torch.randperm(n, device=self.device, generator=self.generator)
-        mb = n // nmb
-        if self._fused_ok(mb):
+        sizes = self.minibatch_sizes(n)
+        mb, nmb = sizes[0], len(sizes)
+        if len(set(sizes)) == 1 and self._fused_ok(mb):
             F = self._fused_for(mb, nmb, n)
             F_adv, F_ret, F_perm = self._static_bufs
             F_adv.copy_(adv)
@@ -513,11 +515,31 @@ class PPOAgent:
             F_perm.copy_(perm)
             rows = F.run(states, pre_tanh, old_lp, F_adv, F_ret, F_perm)
         else:
-            batches = [perm[i * mb:(i + 1) * mb] for i in range(nmb)]  # one partition, all epochs
+            # one partition for all epochs (ppo/agent.py:205); a short last minibatch takes the
+            # reference's ragged path (eager torch steps at the exact sizes)
+            starts = np.cumsum([0] + sizes)
+            batches = [perm[int(starts[i]):int(starts[i + 1])] for i in range(nmb)]
             rows = self._run_epochs(states, pre_tanh, old_lp, adv, ret, batches)
+        self.updates += 1
         if not return_metrics:
             return rows
-        return self._finish_metrics(rows.cpu().numpy(), [mb] * nmb, buf.values.reshape(n), ret)
+        return self._finish_metrics(rows.cpu().numpy(), sizes, buf.values.reshape(n), ret)
+
+    def minibatch_sizes(self, n: int) -> List[int]:
+        """The minibatch partition of an n-sample update; every sample is used once per epoch.
+
+        ``num_minibatches`` set: that many near-equal minibatches (the first n % nmb one row
+        larger).  Otherwise the reference's get_batches partition (ppo/agent.py:140-146):
+        ``batch_size`` rows each and a short last minibatch when batch_size does not divide n."""
+        if self.num_minibatches:
+            nmb = max(1, min(int(self.num_minibatches), n))
+            q, r = divmod(n, nmb)
+            sizes = [q + 1] * r + [q] * (nmb - r)
+        else:
+            bs = max(1, int(self.batch_size))
+            sizes = [bs] * (n // bs) + ([n % bs] if n % bs else [])
+        assert sum(sizes) == n, (sizes, n)
+        return sizes
 
     # ------------------------------------------------------------------ fused HIP step
     def _fused_ok(self, mb: int) -> bool:
@@ -535,6 +557,8 @@ class PPOAgent:
 
         F = self._fused
         if F is None or F.mb != mb or F.nmb != nmb or F.metrics.shape[0] != self.epochs * nmb:
+            if F is not None:  # carry Adam's moments and step count over to the new instance
+                F.export_torch_state()
             F = FusedPPO(self, mb, nmb, group=self._dist, use_graphs=self.use_graphs)
             self._fused = F
             self._learner = None

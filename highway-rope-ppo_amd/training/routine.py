@@ -76,7 +76,27 @@ def _eval_env_like(env, num_episodes: int):
     return ev
 
 
+def _eval_key(agent, num_episodes, exp_seed):
+    """Identity of a deterministic evaluation: the same weights (no update since, no torch-side
+    parameter write) on the same seeds give the same return, bit for bit."""
+    params = tuple((p.data_ptr(), p._version) for p in agent.actor_critic.parameters())
+    return (getattr(agent, "updates", None), params, num_episodes, exp_seed)
+
+
 def _evaluate_vector(env, agent, num_episodes, exp_seed):
+    # With thousands of lockstep envs many eval points (every eval_interval completed episodes)
+    # fall between two updates; the evaluation is deterministic, so a repeat at unchanged
+    # weights reuses the last result instead of re-running the episodes.
+    key = _eval_key(agent, num_episodes, exp_seed)
+    memo = getattr(env.unwrapped, "_eval_memo", None)
+    if memo is not None and memo[0] == key and key[0] is not None:
+        return memo[1]
+    r = _run_eval_vector(env, agent, num_episodes, exp_seed)
+    env.unwrapped._eval_memo = (key, r)
+    return r
+
+
+def _run_eval_vector(env, agent, num_episodes, exp_seed):
     cache = getattr(env.unwrapped, "_eval_envs", None)
     if cache is None:
         cache = {}

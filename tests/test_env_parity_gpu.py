@@ -231,12 +231,21 @@ def test_equal_positions_and_nan():
         hip.close()
 
 
-@pytest.mark.parametrize("E,N,order,pe,d", [(4096, None, "sorted", _abi.PE_NONE, 0),
-                                            (16384, 30, "shuffled", _abi.PE_ROPE, 4)])
+_FULL_SIZE = [(4096, None, "sorted", _abi.PE_NONE, 0),      # configs[1]
+              (16384, 30, "shuffled", _abi.PE_ROPE, 4),   # configs[2] (rotate_dim 4: d <= F)
+              (8192, None, "sorted", _abi.PE_NONE, 0)]    # configs[3]: one GPU's slice of 65536
+# configs[4]: 32768 envs per GPU, 30 observed vehicles, the full PE sweep (d_embed 4 <= F)
+_FULL_SIZE += [(32768, 30, order, pe, 0 if pe == _abi.PE_NONE else 4)
+               for order in ("sorted", "shuffled")
+               for pe in (_abi.PE_NONE, _abi.PE_RANK, _abi.PE_DIST, _abi.PE_ROPE)]
+
+
+@pytest.mark.parametrize("E,N,order,pe,d", _FULL_SIZE)
 def test_full_size_env_blocks_match_oracle(E, N, order, pe, d):
-    """BASELINE configs[1] / configs[2] at full size: the whole batch steps on the GPU with
-    autoreset, and three 16-env blocks (start, middle, end) are replayed on the oracle from the
-    GPU's reset state with the blocks' global env indices (env_offset) -- every word equal."""
+    """BASELINE configs[1] / [2] / [3] (per-GPU slice) / [4] (per-GPU slice, every PE kind and
+    order) at full size: the whole batch steps on the GPU with autoreset, and three 16-env
+    blocks (start, middle, end) are replayed on the oracle from the GPU's reset state with the
+    blocks' global env indices (env_offset) -- every word equal."""
     cfg = make_cfg(E=E, order=order, pe=pe, d=d, N=N)
     table = pe_table_for(pe, d, cfg.obs_vehicles) if pe != _abi.PE_NONE else None
     hip = HipEnv(cfg, table)
@@ -270,3 +279,28 @@ def test_full_size_env_blocks_match_oracle(E, N, order, pe, d):
             np.testing.assert_array_equal(rh[3][off:off + B].astype(bool), ro[3])
         d_ = diff_state(st_end[:, off:off + B, :], ora.state, V)
         assert d_ is None, f"block {off}: {d_}"
+
+
+@pytest.mark.parametrize("E", [4096, 32768])
+def test_hip_reset_layout_known_answer(E):
+    """The HIP reset at full size against upstream create_random's numbers (the oracle-side
+    KAT is tests/test_oracle_env.py::test_reset_layout_known_answer_create_random): every gap
+    within offset * [0.9, 1.1] and the sample spanning that range; speeds 25 / U[21, 24)."""
+    cfg = make_cfg(E=E, autoreset=False)
+    hip = HipEnv(cfg)
+    try:
+        hip.reset()
+        st = hip.state()
+    finally:
+        hip.close()
+    V = cfg.vehicles_count + 1
+    x = st[_abi.F_X, :, :V].view(np.float32).astype(np.float64)
+    spd = st[_abi.F_SPEED, :, :V].view(np.float32).astype(np.float64)
+    spacing = np.full(V, 0.5)
+    spacing[0] = 2.0
+    offset = spacing[None, :] * (12.0 + spd) * np.exp(-5.0 / 40.0 * cfg.lanes_count)
+    prev = np.concatenate([3.0 * offset[:, :1], np.maximum.accumulate(x, axis=1)[:, :-1]], 1)
+    j = (x - prev) / offset
+    assert j.min() >= 0.9 - 2e-4 and j.max() <= 1.1 + 2e-4, (j.min(), j.max())
+    assert j.min() < 0.901 and j.max() > 1.099
+    assert np.all(spd[:, 0] == 25.0) and spd[:, 1:].min() >= 21.0 and spd[:, 1:].max() < 24.0

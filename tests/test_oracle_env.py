@@ -41,6 +41,39 @@ def test_reset_traffic_layout():
     np.testing.assert_allclose(timer, want, atol=2e-4)
 
 
+def test_reset_layout_known_answer_create_random():
+    """Pins the traffic layout to upstream's numbers over 1024 seeds (SURVEY.md §8 a1.9 and the
+    constant table in DESIGN.md §4): ego speed 25 on spacing ego_spacing = 2, others speed
+    U(0.7, 0.8) x speed_limit 30 on spacing 1 / vehicles_density = 0.5; offset =
+    spacing * (12 + v) * exp(-5/40 * lanes); the ego at 3*offset + offset*U(0.9, 1.1), every
+    other car at max(x so far) + offset*U(0.9, 1.1) (highway-env 1.10.1
+    vehicle/kinematics.py Vehicle.create_random: ``x0 += offset * road.np_random.uniform(0.9,
+    1.1)``; SURVEY's a1.9 row quotes (0.95, 1.05), an erratum recorded there).  The jitter
+    range is checked from both sides: every draw inside [0.9, 1.1] and the sample spanning it,
+    which a U(0.95, 1.05) draw could not."""
+    cfg, env, _ = _fresh(E=1024)
+    V = cfg.vehicles_count + 1
+    x = env.ffield(_abi.F_X)[:, :V].astype(np.float64)
+    y = env.ffield(_abi.F_Y)[:, :V]
+    spd = env.ffield(_abi.F_SPEED)[:, :V].astype(np.float64)
+    lanes = cfg.lanes_count
+    fac = np.exp(-5.0 / 40.0 * lanes)
+    spacing = np.full(V, 1.0 / 2.0)
+    spacing[0] = 2.0
+    offset = spacing[None, :] * (12.0 + spd) * fac
+    prev_max = np.concatenate([3.0 * offset[:, :1], np.maximum.accumulate(x, axis=1)[:, :-1]], 1)
+    jitter = (x - prev_max) / offset
+    tol = 2e-4  # binary32 positions up to ~1.4 km
+    assert jitter.min() >= 0.9 - tol and jitter.max() <= 1.1 + tol, (jitter.min(), jitter.max())
+    assert jitter.min() < 0.905 and jitter.max() > 1.095
+    assert np.all(spd[:, 0] == 25.0)
+    assert spd[:, 1:].min() >= 21.0 and spd[:, 1:].max() < 24.0
+    assert spd[:, 1:].min() < 21.05 and spd[:, 1:].max() > 23.95
+    lane_counts = np.bincount((y[:, :V] / 4.0).astype(np.int64).ravel(), minlength=lanes)
+    assert lane_counts.size == lanes and lane_counts.min() > 0.9 * lane_counts.mean()
+    assert np.all(env.ffield(_abi.F_HEADING)[:, :V] == 0.0)
+
+
 def test_reset_observation_is_normalised_relative_sorted():
     cfg, env, obs = _fresh()
     # ego row: absolute x clipped to 1, y = lane/25, vx = 25/30

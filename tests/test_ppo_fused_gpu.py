@@ -51,7 +51,10 @@ def _torch_grad(agent, s, z, lp, adv, ret, idx):
 
 
 @pytest.mark.parametrize("S,H,mb", [(60, 256, 4096), (60, 64, 256), (120, 512, 256), (136, 128, 128),
-                                    (60, 192, 200), (30, 128, 256)])  # last: split-K path (S % 4)
+                                    (60, 192, 200), (30, 128, 256),  # split-K path (S % 4)
+                                    # configs[4]'s learner shapes: N=30 rows of F_out 4 (none /
+                                    # RoPE) or 8 (RankPE / DistPE, d 4), hidden 256 / 384 / 512
+                                    (120, 384, 4096), (240, 256, 4096), (240, 512, 4096)])
 def test_fused_gradient_matches_autograd(S, H, mb):
     a, b = _agents(S, H)
     n = mb * 2
@@ -95,6 +98,153 @@ def test_fused_update_matches_torch_update(graphs):
         assert (d > 2e-5).float().mean().item() < 0.05, (k, d.max().item())
     torch.testing.assert_close(rows_b, rows_a, rtol=5e-3, atol=5e-5)
     assert int(F.counters[0]) == steps
+
+
+def test_fused_update_gradients_match_autograd_every_step():
+    """Every minibatch step of a 3-epoch fused update (graph path) compared at the gradient
+    level: before each step the torch model takes the fused weights, autograd computes the
+    reference gradient (ppo/agent.py:216-248) on that step's minibatch, and the fused gradient
+    must agree elementwise at the single-step tolerance.  Weights never drift apart, so the
+    bound stays as tight as the one-step test over the whole trajectory (Adam's own arithmetic
+    is pinned separately by test_fused_optimizer_matches_torch_adam_on_identical_grads)."""
+    S, H, n, nmb, epochs = 60, 256, 2048, 4, 3
+    a, b = _agents(S, H, epochs=epochs)
+    s, z, lp, adv, ret, perm = _data(n, S, a)
+    mb = n // nmb
+    F = FusedPPO(b, mb, nmb, use_graphs=False)
+    idxs = [perm[i * mb:(i + 1) * mb].contiguous() for i in range(nmb)]
+    args = [F._args(s, z, lp, adv, ret, ix.data_ptr()) for ix in idxs]
+    F.counters.zero_()
+    F.sync_params(args[0])
+    pa = dict(a.actor_critic.named_parameters())
+    pb = dict(b.actor_critic.named_parameters())
+    worst = 0.0
+    for step in range(epochs * nmb):
+        i = step % nmb
+        with torch.no_grad():
+            for name in pa:
+                pa[name].copy_(pb[name])
+        g_ref, m_ref = _torch_grad(a, s, z, lp, adv, ret, idxs[i])
+        F._fwd_bwd(args[i])
+        torch.cuda.synchronize()
+        for name in pa:
+            ref = pa[name].grad
+            scale = max(ref.abs().max().item(), 1e-3)
+            torch.testing.assert_close(pb[name].grad, ref, rtol=1e-3, atol=2e-5 * scale,
+                                       msg=f"step {step} {name}")
+            worst = max(worst, ((pb[name].grad - ref).abs().max() / scale).item())
+        torch.testing.assert_close(F.metrics[step], m_ref, rtol=1e-4, atol=1e-6)
+        F._opt(args[i])
+    assert int(F.counters[0]) == epochs * nmb
+    assert worst < 2e-4, worst
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_fused_update_replays_reference_golden(graphs):
+    """The reference's own update (tests/golden/ppo_agent.npz 'upd_a': n 256, h64, 2 epochs,
+    batch_size 64, generated from ppo/agent.py:196-308) replayed through the PRODUCT path:
+    PPOAgent.update_rollout -> hwy_gae -> FusedPPO (the HIP minibatch kernels, HIP graphs when
+    graphs=True) with the golden minibatch permutation.  Final weights and metrics match the
+    golden at the torch path's tolerance."""
+    from agent_util import load
+    from ppo.agent import PPOAgent, RolloutBuffer
+
+    g, meta = load()
+    name = "upd_a"
+    m = meta["agent"][name]
+    n, S = m["n"], m["state_dim"]
+    agent = PPOAgent(S, 2, lr=m["lr"], epochs=m["epochs"], batch_size=m["batch_size"],
+                     hidden_dim=m["hidden_dim"], device=DEV, use_graphs=graphs, backend="hip")
+    sd = {k[len(name) + 6:]: torch.as_tensor(g[k]) for k in g.files if k.startswith(f"{name}_init_")}
+    agent.actor_critic.load_state_dict(sd)
+    buf = RolloutBuffer(n, 1, S, 2, DEV)
+    f = lambda k: torch.as_tensor(np.asarray(g[f"{name}_{k}"], np.float32), device=DEV)  # noqa: E731
+    buf.states[:n].copy_(f("states").view(n, 1, S))
+    buf.actions.copy_(f("actions").view(n, 1, 2))
+    buf.pre_tanh.copy_(f("pre_tanh").view(n, 1, 2))
+    buf.log_probs.copy_(f("log_probs").view(n, 1))
+    buf.values.copy_(f("values").view(n, 1))
+    buf.rewards.copy_(f("rewards").view(n, 1))
+    buf.dones.copy_(torch.as_tensor(np.asarray(g[f"{name}_dones"], np.uint8), device=DEV).view(n, 1))
+    perm = torch.as_tensor(np.asarray(g[f"{name}_perm"], np.int64), device=DEV)
+    last = torch.tensor([m["last_value"]], dtype=torch.float32, device=DEV)
+    metrics = agent.update_rollout(buf, last, perm=perm)
+    assert agent._fused is not None and agent._fused.mb == 64 and agent._fused.nmb == n // 64
+    for k, v in agent.actor_critic.state_dict().items():
+        np.testing.assert_allclose(v.detach().cpu().numpy(), g[f"{name}_final_{k}"], atol=5e-5,
+                                   rtol=5e-5, err_msg=k)
+    for k, want in m["metrics"].items():
+        assert abs(metrics[k] - want) <= 1e-4 * max(1.0, abs(want)), (k, metrics[k], want)
+
+
+def test_ragged_update_rollout_replays_reference_golden():
+    """'upd_b' (n 130, batch_size 50: minibatches 50 / 50 / 30) through update_rollout: the
+    reference's get_batches partition with its short last minibatch is kept (no sample is
+    dropped) and the result matches the golden."""
+    from agent_util import load
+    from ppo.agent import PPOAgent, RolloutBuffer
+
+    g, meta = load()
+    name = "upd_b"
+    m = meta["agent"][name]
+    n, S = m["n"], m["state_dim"]
+    agent = PPOAgent(S, 2, lr=m["lr"], epochs=m["epochs"], batch_size=m["batch_size"],
+                     hidden_dim=m["hidden_dim"], device=DEV, use_graphs=False)
+    assert agent.minibatch_sizes(n) == [50, 50, 30]
+    sd = {k[len(name) + 6:]: torch.as_tensor(g[k]) for k in g.files if k.startswith(f"{name}_init_")}
+    agent.actor_critic.load_state_dict(sd)
+    buf = RolloutBuffer(n, 1, S, 2, DEV)
+    f = lambda k: torch.as_tensor(np.asarray(g[f"{name}_{k}"], np.float32), device=DEV)  # noqa: E731
+    buf.states[:n].copy_(f("states").view(n, 1, S))
+    buf.pre_tanh.copy_(f("pre_tanh").view(n, 1, 2))
+    buf.log_probs.copy_(f("log_probs").view(n, 1))
+    buf.values.copy_(f("values").view(n, 1))
+    buf.rewards.copy_(f("rewards").view(n, 1))
+    buf.dones.copy_(torch.as_tensor(np.asarray(g[f"{name}_dones"], np.uint8), device=DEV).view(n, 1))
+    perm = torch.as_tensor(np.asarray(g[f"{name}_perm"], np.int64), device=DEV)
+    last = torch.tensor([m["last_value"]], dtype=torch.float32, device=DEV)
+    metrics = agent.update_rollout(buf, last, perm=perm)
+    for k, v in agent.actor_critic.state_dict().items():
+        np.testing.assert_allclose(v.detach().cpu().numpy(), g[f"{name}_final_{k}"], atol=5e-5,
+                                   rtol=5e-5, err_msg=k)
+    for k, want in m["metrics"].items():
+        assert abs(metrics[k] - want) <= 1e-4 * max(1.0, abs(want)), (k, metrics[k], want)
+
+
+def test_fused_rebuild_carries_adam_state():
+    """Changing the minibatch geometry rebuilds FusedPPO; Adam's moments and step count carry
+    over: a rebuilt instance continues exactly where the old one stopped."""
+    S, H = 60, 64
+    a, b = _agents(S, H)
+    s, z, lp, adv, ret, perm = _data(512, S, a)
+    b.num_minibatches = 4
+    F1 = b._fused_for(128, 4, 512)
+    F1.run(s, z, lp, adv.clone(), ret.clone(), perm.clone())
+    m1, v1, t1 = F1.m.clone(), F1.v.clone(), int(F1.counters[0])
+    F2 = b._fused_for(256, 2, 512)
+    assert F2 is not F1
+    torch.cuda.synchronize()
+    assert int(F2.counters[0]) == t1 == 8
+    assert torch.equal(F2.m, m1) and torch.equal(F2.v, v1)
+
+
+def test_fused_graph_recaptures_on_hyperparameter_change():
+    """The epoch graph bakes lr / eps_clip / coefficients into its kernel arguments: changing
+    them between updates recaptures, so the graph path equals the eager path after the change."""
+    S, H, n, nmb = 60, 64, 512, 4
+    outs = []
+    for graphs in (False, True):
+        a, b = _agents(S, H, graphs=graphs)
+        s, z, lp, adv, ret, perm = _data(n, S, a)
+        F = FusedPPO(b, n // nmb, nmb, use_graphs=graphs)
+        F.run(s, z, lp, adv, ret, perm)
+        for grp in b.optimizer.param_groups:
+            grp["lr"] = 1e-3
+        b.eps_clip, b.entropy_coef = 0.1, 0.02
+        F.run(s, z, lp, adv, ret, perm)
+        torch.cuda.synchronize()
+        outs.append(F.flat.clone())
+    assert torch.equal(outs[0], outs[1])
 
 
 def test_fused_optimizer_matches_torch_adam_on_identical_grads():

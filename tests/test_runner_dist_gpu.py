@@ -55,7 +55,8 @@ def _worker(rank, world, port, out_dir):
     out = {"status": res["status"], "error": res.get("error_message"), "rank": res.get("rank", 0),
            "episodes": mh.get("episode_numbers", []), "updates": len(mh.get("policy_updates", [])),
            "evals": len(res.get("rewards", [])), "wsum": float(w.double().sum()),
-           "wabs": float(w.double().abs().sum())}
+           "wabs": float(w.double().abs().sum()),
+           "gen_seed": int(agent_box["a"].generator.initial_seed())}
     with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
         json.dump(out, f)
     torch.distributed.destroy_process_group()
@@ -73,6 +74,9 @@ def test_runner_one_experiment_over_two_ranks(tmp_path):
     assert r0["episodes"] == r1["episodes"] == list(range(1, EPISODES + 1))
     assert r0["updates"] == r1["updates"] >= 1
     assert r0["wsum"] == r1["wsum"] and r0["wabs"] == r1["wabs"]  # replicas identical
+    # each rank samples its envs' exploration noise from its own stream (the same
+    # stream on every rank would give global env r*E+e the noise of env e)
+    assert r0["gen_seed"] != r1["gen_seed"]
     assert r0["evals"] == 1 + EPISODES // 50 and r1["evals"] == 0
     assert (tmp_path / "cwd0/artifacts/highway-ppo/summary_dist_runner.csv").exists()
     assert not (tmp_path / "cwd1/artifacts/highway-ppo/summary_dist_runner.csv").exists()

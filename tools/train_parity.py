@@ -13,6 +13,9 @@ seed 42 136.8270, 1042 127.8022, 2042 132.6172; mean 132.42).
 Usage (GPU box):  python tools/train_parity.py --seeds 42 --out gpurun_out/train
     --num-envs 1   the reference's own loop (1 env, batch-1 select_action, 2048-step updates)
     --num-envs E   the lockstep loop (E envs, same hyperparameters, same episode budget)
+    --num-envs E --rollout T --minibatches M
+                   the many-env recipe: steps_per_update = E*T, M minibatches per epoch (the
+                   bench's configs[1] recipe is E 4096, T 32, M 32), --episodes sets the budget
 Under torchrun (--nproc-per-node N) each experiment spans the N GPUs with E envs per rank
 (experiments/runner.py); rank 0 prints and writes the summary.
 """
@@ -45,6 +48,12 @@ def main():
     p.add_argument("--num-envs", type=int, default=1)
     p.add_argument("--out", default="gpurun_out/train")
     p.add_argument("--condition", default="sorted", choices=sorted(REFERENCE_FINAL))
+    p.add_argument("--rollout", type=int, default=0,
+                   help="rollout steps per env per update (0: ceil(2048 / num_envs))")
+    p.add_argument("--minibatches", type=int, default=0, help="minibatches per epoch (0: n / 64)")
+    p.add_argument("--eval-interval", type=int, default=50)
+    p.add_argument("--lr", type=float, default=3e-4)
+    p.add_argument("--epochs", type=int, default=8)
     args = p.parse_args()
 
     out = os.path.abspath(args.out)
@@ -61,15 +70,20 @@ def main():
             "shuffled_rankpe": Condition.SHUFFLED_RANKPE}[args.condition]
     d_embed = None if args.condition == "sorted" else 4
     for seed in args.seeds:
-        name = (f"{args.condition}_lr0.0003_hidden_dim256_clip_eps0.2_entropy_coef0.005_epochs8_"
-                f"batch_size64" + (f"_d_embed{d_embed}" if d_embed else "") + f"_seed{seed}"
-                + (f"_envs{args.num_envs}" if args.num_envs > 1 else ""))
-        hp = ConditionHP(lr=3e-4, clip_eps=0.2, epochs=8, batch_size=64, hidden_dim=256,
-                         d_embed=d_embed)
+        name = (f"{args.condition}_lr{args.lr:g}_hidden_dim256_clip_eps0.2_entropy_coef0.005_"
+                f"epochs{args.epochs}_batch_size64" + (f"_d_embed{d_embed}" if d_embed else "")
+                + f"_seed{seed}" + (f"_envs{args.num_envs}" if args.num_envs > 1 else "")
+                + (f"_T{args.rollout}_mb{args.minibatches}" if args.rollout else ""))
+        hp = ConditionHP(lr=args.lr, clip_eps=0.2, epochs=args.epochs, batch_size=64,
+                         hidden_dim=256, d_embed=d_embed)
         hp.entropy_coef = 0.005
-        extra = {"log_interval": 50, "eval_interval": 50}
+        if args.rollout:
+            hp.steps_per_update = args.num_envs * args.rollout
+        extra = {"log_interval": 50, "eval_interval": args.eval_interval}
         if args.num_envs > 1:
             extra["num_envs"] = args.num_envs
+        if args.minibatches:
+            extra["num_minibatches"] = args.minibatches
         exp = Experiment(name=name, condition=cond, hp=hp, seed=seed,
                          max_episodes=args.episodes, target_reward=130.0, extra=extra)
         run_dir = os.path.join(out, f"{args.condition}_seed{seed}")
@@ -83,13 +97,19 @@ def main():
             os.chdir(cwd)
         wall = time.time() - t0
         row = {"condition": args.condition, "seed": seed, "experiment": name, "status": res["status"], "wall_s": round(wall, 1),
-               "num_envs": args.num_envs, "episodes": args.episodes,
+               "num_envs": args.num_envs, "episodes": args.episodes, "rollout": args.rollout,
+               "minibatches": args.minibatches, "eval_interval": args.eval_interval,
+               "lr": args.lr, "epochs": args.epochs,
                "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else "cpu"}
         if res["status"] == "COMPLETED":
             avg = res["avg_rewards"]
             hist = res["metrics_history"]
+            ups = hist.get("policy_updates", [])
             row.update(final_reward=round(float(avg[-1]), 4), max_reward=round(float(max(avg)), 4),
-                       evals=[round(float(x), 2) for x in hist.get("eval_rewards", [])])
+                       evals=[round(float(x), 2) for x in hist.get("eval_rewards", [])],
+                       eval_episodes=hist.get("eval_episode_numbers", []),
+                       env_steps=int(sum(u.get("steps", 0) for u in ups)), updates=len(ups),
+                       train_s=round(float(sum(u.get("time", 0.0) for u in ups)), 2))
             ref = REFERENCE_FINAL[args.condition].get(seed)
             if ref is not None:
                 row.update(reference_final_reward=ref,
