@@ -396,36 +396,37 @@ class PPOAgent:
         return ok
 
     # ------------------------------------------------------------------ metrics
-    def _finish_metrics(self, rows: np.ndarray, sizes: List[int], values, returns) -> Dict[str, float]:
+    def _finish_metrics(self, rows: torch.Tensor, sizes: List[int], values, returns) -> Dict[str, float]:
         """Aggregate per-minibatch rows like ppo/agent.py:263-287 (epoch means, then the mean
-        over epochs, in float64) plus explained variance (:272-280)."""
+        over epochs, in float64) plus explained variance (:272-280).  Computed on the rows'
+        device with one host transfer at the end (the clip count becomes a fraction by dividing
+        by each minibatch's size, as the reference's per-batch clip_frac)."""
         nb = len(sizes)
-        totals = dict.fromkeys(METRIC_KEYS, 0.0)
+        r = torch.as_tensor(rows).to(torch.float64)[: self.epochs * nb].view(self.epochs, nb, -1)
         ci = METRIC_KEYS.index("clip_fraction")
-        for e in range(self.epochs):
-            blk = rows[e * nb:(e + 1) * nb]
-            for j, k in enumerate(METRIC_KEYS):
-                s = 0.0
-                for b in range(nb):
-                    v = float(blk[b, j])
-                    s += v / sizes[b] if j == ci else v
-                totals[k] += s / nb
+        inv = torch.tensor([1.0 / s for s in sizes], dtype=torch.float64, device=r.device)
+        r = torch.cat([r[..., :ci], r[..., ci:ci + 1] * inv.view(1, nb, 1), r[..., ci + 1:]], -1)
+        means = r.mean(dim=1).mean(dim=0)  # epoch means, then over epochs
         with torch.no_grad():
             var_y = torch.var(returns)
-            ev = (1 - torch.var(returns - values) / var_y).item() if var_y.item() > 0 else 0.0
+            ev = torch.where(var_y > 0, 1 - torch.var(returns - values) / var_y,
+                             torch.zeros_like(var_y)).to(torch.float64).to(means.device)
+        vals = torch.cat([means, ev.view(1)]).tolist()
+        m = dict(zip(METRIC_KEYS, vals[:-1]))
         out = {
-            "loss": totals["loss"] / self.epochs,
-            "policy_loss": totals["policy_loss"] / self.epochs,
-            "value_loss": totals["value_loss"] / self.epochs,
-            "entropy": totals["entropy"] / self.epochs,
-            "clip_fraction": totals["clip_fraction"] / self.epochs,
-            "approx_kl": totals["approx_kl"] / self.epochs,
-            "explained_variance": ev,
+            "loss": m["loss"],
+            "policy_loss": m["policy_loss"],
+            "value_loss": m["value_loss"],
+            "entropy": m["entropy"],
+            "clip_fraction": m["clip_fraction"],
+            "approx_kl": m["approx_kl"],
+            "explained_variance": vals[-1],
         }
         self.logger.info(
             "update_complete loss=%.4f policy_loss=%.4f value_loss=%.4f entropy=%.4f "
             "clip_frac=%.3f kl=%.5f explained_var=%.3f", out["loss"], out["policy_loss"],
-            out["value_loss"], out["entropy"], out["clip_fraction"], out["approx_kl"], ev)
+            out["value_loss"], out["entropy"], out["clip_fraction"], out["approx_kl"],
+            out["explained_variance"])
         return out
 
     def _learner_for(self, n: int, mb: int, steps: int, graph: bool) -> _Learner:
@@ -470,7 +471,7 @@ class PPOAgent:
         batches = [torch.as_tensor(b, device=self.device) for b in self.memory.get_batches()]
         rows = self._run_epochs(states, pre_tanh, old_log_probs, advantages, returns, batches)
         values = torch.as_tensor(np.asarray(self.memory.values, np.float32), device=self.device)
-        out = self._finish_metrics(rows.cpu().numpy(), [int(b.numel()) for b in batches], values,
+        out = self._finish_metrics(rows, [int(b.numel()) for b in batches], values,
                                    returns)
         self.memory.clear()
         self.updates += 1
@@ -523,7 +524,7 @@ class PPOAgent:
         self.updates += 1
         if not return_metrics:
             return rows
-        return self._finish_metrics(rows.cpu().numpy(), sizes, buf.values.reshape(n), ret)
+        return self._finish_metrics(rows, sizes, buf.values.reshape(n), ret)
 
     def minibatch_sizes(self, n: int) -> List[int]:
         """The minibatch partition of an n-sample update; every sample is used once per epoch.

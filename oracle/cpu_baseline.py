@@ -25,7 +25,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def _worker(args):
-    seed, steps, steps_per_update, hidden, epochs, batch_size, q = args
+    seed, steps, steps_per_update, hidden, epochs, batch_size, lr, q = args
     os.environ["OMP_NUM_THREADS"] = "1"
     import torch
     import torch.nn as nn
@@ -57,7 +57,7 @@ def _worker(args):
     torch.manual_seed(seed)
     np.random.seed(seed)
     ac = AC()
-    opt = torch.optim.Adam(ac.parameters(), lr=3e-4)
+    opt = torch.optim.Adam(ac.parameters(), lr=lr)
     obs = env.reset()
     S, Z, LP, R, D, V = [], [], [], [], [], []
     done_steps = 0
@@ -116,12 +116,12 @@ def _worker(args):
 
 
 def run(procs: int = 4, steps: int = 2048, steps_per_update: int = 2048, hidden: int = 256,
-        epochs: int = 8, batch_size: int = 64) -> dict:
+        epochs: int = 8, batch_size: int = 64, lr: float = 3e-4) -> dict:
     """Time `procs` independent reference-structure training processes; returns a summary."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     ps = [ctx.Process(target=_worker, args=((42 + 1000 * i, steps, steps_per_update, hidden, epochs,
-                                            batch_size, q),)) for i in range(procs)]
+                                            batch_size, lr, q),)) for i in range(procs)]
     for p in ps:
         p.start()
     res = [q.get() for _ in ps]

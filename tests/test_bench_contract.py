@@ -34,5 +34,25 @@ def test_cli_defaults(monkeypatch):
     b = _bench()
     monkeypatch.setattr(sys, "argv", ["bench.py"])
     a = b.parse()
-    assert (a.gpus, a.steps, a.warmup, a.envs, a.hidden, a.epochs, a.minibatches) == \
-        (1, 5, 2, 4096, 256, 8, 32)
+    assert (a.gpus, a.steps, a.warmup, a.config, a.hidden, a.epochs, a.minibatches) == \
+        (1, 5, 2, 1, 256, 8, 32)
+    assert b.CONFIGS[1] == dict(envs=4096, obs=15, order="sorted", pe="none", d=0)
+
+
+def test_config_table_matches_baseline_json():
+    """--config N is BASELINE.json's configs[N] per GPU (configs[3]: 65536 / 8 GPUs)."""
+    import json
+
+    b = _bench()
+    cfgs = json.load(open(os.path.join(ROOT, "BASELINE.json")))["configs"]
+    assert "4096" in cfgs[1] and b.CONFIGS[1]["envs"] == 4096
+    assert "16384" in cfgs[2] and "30 vehicles" in cfgs[2] and "RoPE" in cfgs[2]
+    assert (b.CONFIGS[2]["envs"], b.CONFIGS[2]["obs"], b.CONFIGS[2]["pe"]) == (16384, 30, "rope")
+    assert "65536" in cfgs[3] and b.CONFIGS[3]["envs"] * 8 == 65536
+    assert "32768" in cfgs[4] and (b.CONFIGS[4]["envs"], b.CONFIGS[4]["obs"]) == (32768, 30)
+
+
+def test_cpu_share_is_bounded_by_the_machine():
+    b = _bench()
+    c = b.cpu_share()
+    assert 1 <= c["share"] <= c["os_cpu_count"] and c["affinity"] <= c["os_cpu_count"]

@@ -137,3 +137,58 @@ def test_rccl_captured_allreduce_matches_stepwise_and_local(tmp_path):
         # partial sums round differently from ppo_wsum's
         torch.testing.assert_close(r["captured"]["state"][k], r["local"]["state"][k], rtol=1e-4,
                                    atol=1e-6)
+
+
+def _refusal_worker(rank, world, port, out_dir, refuse):
+    """capture_collectives forced on over gloo; with `refuse` the first collective inside the
+    capture raises (as a refused RCCL capture would), so FusedPPO must fall back to per-step
+    graphs with the all-reduce between them."""
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.join(os.path.dirname(here), "highway-rope-ppo_amd"), here]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    from hwy.ppo_native import FusedPPO
+
+    group = torch.distributed.group.WORLD
+    agent = _agent(dev, group)
+    d = _data(rank, dev)
+    adv = agent.normalize_advantages(d["a"])
+    F = FusedPPO(agent, NLOC // NMB, NMB, group=group, use_graphs=True)
+    tried = {"n": 0}
+    if refuse:
+        F.capture_collectives = True
+        real = F._allreduce
+
+        def _allreduce():
+            if torch.cuda.is_current_stream_capturing():
+                tried["n"] += 1
+                raise RuntimeError("collective capture refused (test)")
+            real()
+
+        F._allreduce = _allreduce
+    for _ in range(2):  # a second update replays the fallback graphs
+        F.run(d["s"], d["z"].contiguous(), d["lp"], adv.contiguous(), d["r"], d["perm"])
+    torch.cuda.synchronize()
+    torch.save({"state": {k: v.cpu() for k, v in agent.actor_critic.state_dict().items()},
+                "tried": tried["n"], "captured": F._captured_collectives,
+                "capture_flag": F.capture_collectives},
+               os.path.join(out_dir, f"{'refused' if refuse else 'plain'}{rank}.pt"))
+    torch.distributed.destroy_process_group()
+
+
+def test_refused_collective_capture_falls_back_to_per_step_graphs(tmp_path):
+    """a refused capture of the epoch graph with its collectives falls back to
+    per-step graphs with the all-reduce issued between them; the fallback's weights equal the
+    HWY_GRAPH_COLLECTIVES=0 path's bit for bit on every rank."""
+    for refuse in (False, True):
+        mp.start_processes(_refusal_worker, args=(2, _free_port(), str(tmp_path), refuse),
+                           nprocs=2, join=True, start_method="spawn")
+    for r in range(2):
+        a = torch.load(tmp_path / f"plain{r}.pt", weights_only=True)
+        b = torch.load(tmp_path / f"refused{r}.pt", weights_only=True)
+        assert b["tried"] == 1 and not b["captured"] and not b["capture_flag"]
+        for k in a["state"]:
+            assert torch.equal(a["state"][k], b["state"][k]), (r, k)

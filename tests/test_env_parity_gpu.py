@@ -303,4 +303,5 @@ def test_hip_reset_layout_known_answer(E):
     j = (x - prev) / offset
     assert j.min() >= 0.9 - 2e-4 and j.max() <= 1.1 + 2e-4, (j.min(), j.max())
     assert j.min() < 0.901 and j.max() > 1.099
-    assert np.all(spd[:, 0] == 25.0) and spd[:, 1:].min() >= 21.0 and spd[:, 1:].max() < 24.0
+    # U(21, 24) in binary32: 21 + 3 * (1 - 2^-24) rounds to 24.0
+    assert np.all(spd[:, 0] == 25.0) and spd[:, 1:].min() >= 21.0 and spd[:, 1:].max() <= 24.0

@@ -40,6 +40,27 @@ def _data(n, S, agent, seed=1):
     return s, z.contiguous(), lp.contiguous(), adv, ret, perm
 
 
+def _grad64(agent, s, z, lp, adv, ret, idx):
+    """The same minibatch loss and gradient (ppo/agent.py:216-248) in float64 autograd."""
+    import copy
+
+    import torch.nn.functional as Fn
+    from torch.distributions import Normal
+
+    ag = agent
+    m = copy.deepcopy(ag.actor_critic).double()
+    s, z, lp, adv, ret = (t.double()[idx] for t in (s, z, lp, adv, ret))
+    mean, std, v = m(s)
+    dist = Normal(mean, std, validate_args=False)
+    nlp = (dist.log_prob(z) - torch.log1p(-torch.tanh(z).pow(2) + 1e-6)).sum(-1)
+    r = torch.exp(nlp - lp)
+    loss = (-torch.min(r * adv, torch.clamp(r, 1 - ag.eps_clip, 1 + ag.eps_clip) * adv).mean()
+            + ag.value_coef * Fn.mse_loss(v.squeeze(-1), ret)
+            - ag.entropy_coef * dist.entropy().sum(-1).mean())
+    loss.backward()
+    return {n: p.grad for n, p in m.named_parameters()}
+
+
 def _torch_grad(agent, s, z, lp, adv, ret, idx):
     from ppo.agent import _Learner
 
@@ -56,10 +77,16 @@ def _torch_grad(agent, s, z, lp, adv, ret, idx):
                                     # RoPE) or 8 (RankPE / DistPE, d 4), hidden 256 / 384 / 512
                                     (120, 384, 4096), (240, 256, 4096), (240, 512, 4096)])
 def test_fused_gradient_matches_autograd(S, H, mb):
+    """One fused forward/backward against autograd on the same minibatch.  The reference
+    gradient is float64 autograd: at S = 240 / H = 512 and 4096 rows torch's own fp32 GEMMs
+    are off by up to 1.7e-6 on near-cancelling sums (tools/r2/probe_grad_f64.py, where the
+    fused kernel stays within 7e-10), so fp32 torch is no longer the tighter reference.  The
+    fused result must also be at least as close to float64 as torch fp32 is, up to rounding."""
     a, b = _agents(S, H)
     n = mb * 2
     s, z, lp, adv, ret, perm = _data(n, S, a)
     idx = perm[:mb].contiguous()
+    g64 = _grad64(a, s, z, lp, adv, ret, idx)
     g_ref, m_ref = _torch_grad(a, s, z, lp, adv, ret, idx)
     F = FusedPPO(b, mb, 2, use_graphs=False)
     args = F._args(s, z, lp, adv, ret, idx.data_ptr())
@@ -70,9 +97,13 @@ def test_fused_gradient_matches_autograd(S, H, mb):
     ga = dict(a.actor_critic.named_parameters())
     gb = dict(b.actor_critic.named_parameters())
     for name, pa in ga.items():
-        ref = pa.grad
+        ref = g64[name]
         scale = max(ref.abs().max().item(), 1e-3)
-        torch.testing.assert_close(gb[name].grad, ref, rtol=1e-3, atol=2e-5 * scale, msg=name)
+        got = gb[name].grad.double()
+        torch.testing.assert_close(got, ref, rtol=1e-3, atol=2e-5 * scale, msg=name)
+        e_fused = (got - ref).abs().max().item()
+        e_torch = (pa.grad.double() - ref).abs().max().item()
+        assert e_fused <= 2 * e_torch + 1e-6 * scale, (name, e_fused, e_torch)
     m = F.metrics[0]
     # policy, value, entropy, loss, clip count, kl
     torch.testing.assert_close(m, m_ref, rtol=1e-4, atol=1e-6)
