@@ -315,6 +315,46 @@ class _Learner:
             self._opt()
 
 
+class _PendingMetrics:
+    """An update's metrics dict whose device-to-host copy is in flight (non-blocking, pinned):
+    result() waits for it, so a caller can enqueue the next rollout before reading them."""
+
+    def __init__(self, logger, vals: torch.Tensor):
+        self.logger = logger
+        self._out = None
+        if vals.is_cuda:
+            self._host = torch.empty(vals.shape, dtype=vals.dtype, pin_memory=True)
+            self._host.copy_(vals, non_blocking=True)
+            self._event = torch.cuda.Event()
+            self._event.record()
+        else:
+            self._host, self._event = vals, None
+
+    def result(self) -> Dict[str, float]:
+        if self._out is not None:
+            return self._out
+        if self._event is not None:
+            self._event.synchronize()
+        vals = self._host.tolist()
+        m = dict(zip(METRIC_KEYS, vals[:-1]))
+        out = {
+            "loss": m["loss"],
+            "policy_loss": m["policy_loss"],
+            "value_loss": m["value_loss"],
+            "entropy": m["entropy"],
+            "clip_fraction": m["clip_fraction"],
+            "approx_kl": m["approx_kl"],
+            "explained_variance": vals[-1],
+        }
+        self.logger.info(
+            "update_complete loss=%.4f policy_loss=%.4f value_loss=%.4f entropy=%.4f "
+            "clip_frac=%.3f kl=%.5f explained_var=%.3f", out["loss"], out["policy_loss"],
+            out["value_loss"], out["entropy"], out["clip_fraction"], out["approx_kl"],
+            out["explained_variance"])
+        self._out = out
+        return out
+
+
 class PPOAgent:
     def __init__(self, state_dim: int, action_dim: int, lr: float = 1e-4, gamma: float = 0.99,
                  lam: float = 0.95, eps_clip: float = 0.2, value_coef: float = 0.5,
@@ -396,11 +436,13 @@ class PPOAgent:
         return ok
 
     # ------------------------------------------------------------------ metrics
-    def _finish_metrics(self, rows: torch.Tensor, sizes: List[int], values, returns) -> Dict[str, float]:
+    def _finish_metrics(self, rows: torch.Tensor, sizes: List[int], values, returns,
+                        deferred: bool = False):
         """Aggregate per-minibatch rows like ppo/agent.py:263-287 (epoch means, then the mean
         over epochs, in float64) plus explained variance (:272-280).  Computed on the rows'
         device with one host transfer at the end (the clip count becomes a fraction by dividing
-        by each minibatch's size, as the reference's per-batch clip_frac)."""
+        by each minibatch's size, as the reference's per-batch clip_frac).  ``deferred``: return
+        a pending result whose host copy is still in flight (see _PendingMetrics)."""
         nb = len(sizes)
         r = torch.as_tensor(rows).to(torch.float64)[: self.epochs * nb].view(self.epochs, nb, -1)
         ci = METRIC_KEYS.index("clip_fraction")
@@ -411,23 +453,8 @@ class PPOAgent:
             var_y = torch.var(returns)
             ev = torch.where(var_y > 0, 1 - torch.var(returns - values) / var_y,
                              torch.zeros_like(var_y)).to(torch.float64).to(means.device)
-        vals = torch.cat([means, ev.view(1)]).tolist()
-        m = dict(zip(METRIC_KEYS, vals[:-1]))
-        out = {
-            "loss": m["loss"],
-            "policy_loss": m["policy_loss"],
-            "value_loss": m["value_loss"],
-            "entropy": m["entropy"],
-            "clip_fraction": m["clip_fraction"],
-            "approx_kl": m["approx_kl"],
-            "explained_variance": vals[-1],
-        }
-        self.logger.info(
-            "update_complete loss=%.4f policy_loss=%.4f value_loss=%.4f entropy=%.4f "
-            "clip_frac=%.3f kl=%.5f explained_var=%.3f", out["loss"], out["policy_loss"],
-            out["value_loss"], out["entropy"], out["clip_fraction"], out["approx_kl"],
-            out["explained_variance"])
-        return out
+        pending = _PendingMetrics(self.logger, torch.cat([means, ev.view(1)]))
+        return pending if deferred else pending.result()
 
     def _learner_for(self, n: int, mb: int, steps: int, graph: bool) -> _Learner:
         L = self._learner
@@ -492,8 +519,11 @@ class PPOAgent:
         return ((adv - mean.float()) / (var.clamp_min(0).sqrt().float() + 1e-8))
 
     def update_rollout(self, buf: RolloutBuffer, last_values: torch.Tensor,
-                       perm: Optional[torch.Tensor] = None, return_metrics: bool = True):
-        """Batched clipped-PPO update on a device rollout (no host round trips until the end)."""
+                       perm: Optional[torch.Tensor] = None, return_metrics=True):
+        """Batched clipped-PPO update on a device rollout (no host round trips until the end).
+        return_metrics: True -> the metrics dict; "deferred" -> a pending result (metrics
+        computed on the device, host copy in flight; .result() gives the dict); False -> the
+        device rows only."""
         from hwy import ops
 
         T, E = buf.T, buf.E
@@ -524,7 +554,8 @@ class PPOAgent:
         self.updates += 1
         if not return_metrics:
             return rows
-        return self._finish_metrics(rows, sizes, buf.values.reshape(n), ret)
+        return self._finish_metrics(rows, sizes, buf.values.reshape(n), ret,
+                                    deferred=return_metrics == "deferred")
 
     def minibatch_sizes(self, n: int) -> List[int]:
         """The minibatch partition of an n-sample update; every sample is used once per epoch.
