@@ -49,6 +49,7 @@
 #define LANE_CHANGE_DELAY 1.0f
 #define PERCEPTION_DISTANCE 200.0f
 #define TWO_SQRT_AB 7.745966692414834f
+#define INV_TWO_SQRT_AB 0.12909944487358056f  // 1 / (2 sqrt(15)), correctly rounded
 #define VEH_DIAGONAL 5.385164807134504f
 
 // ------------------------------------------------------------------------- wave primitives
@@ -209,15 +210,15 @@ __device__ __forceinline__ float desired_gap(float a_spd, float a_c, float a_s, 
                                              float b_c, float b_s) {
   float avx = a_spd * a_c, avy = a_spd * a_s;
   float bvx = b_spd * b_c, bvy = b_spd * b_s;
-  float dv = (avx - bvx) * a_c + (avy - bvy) * a_s;
-  return (DISTANCE_WANTED + a_spd * TIME_WANTED) + (a_spd * dv) / TWO_SQRT_AB;
+  float dv = hm_fma(avx - bvx, a_c, (avy - bvy) * a_s);
+  return hm_fma(a_spd, TIME_WANTED, DISTANCE_WANTED) + (a_spd * dv) * INV_TWO_SQRT_AB;
 }
 
 // IDMVehicle.acceleration, free-road term (depends on the ego vehicle and DELTA only)
 __device__ __forceinline__ float idm_free(float ev_spd, float ev_tsp, float delta, float limit) {
   float tsp = hm_clipf(ev_tsp, 0.0f, limit);
   float base = hm_maxf(ev_spd, 0.0f) / hm_absf(hm_not_zero(tsp));
-  return COMFORT_ACC_MAX * (1.0f - hm_powf(base, delta));
+  return hm_fma(-COMFORT_ACC_MAX, hm_powf(base, delta), COMFORT_ACC_MAX);
 }
 
 // IDMVehicle.acceleration given its free-road term `acc` (interaction with the front vehicle)
@@ -227,7 +228,7 @@ __device__ __forceinline__ float idm_with_front(float acc, float ev_spd, float e
   if (has_front) {
     float d = fv_x - ev_x;
     float g = desired_gap(ev_spd, ev_c, ev_s, fv_spd, fv_c, fv_s) / hm_not_zero(d);
-    acc = acc - COMFORT_ACC_MAX * (g * g);
+    acc = hm_fma(-COMFORT_ACC_MAX, g * g, acc);
   }
   return acc;
 }
@@ -240,7 +241,7 @@ __device__ __forceinline__ float idm_acc(float ev_spd, float ev_tsp, float ev_x,
   if (has_front) {
     float d = fv_x - ev_x;
     float g = desired_gap(ev_spd, ev_c, ev_s, fv_spd, fv_c, fv_s) / hm_not_zero(d);
-    acc = acc - COMFORT_ACC_MAX * (g * g);
+    acc = hm_fma(-COMFORT_ACC_MAX, g * g, acc);
   }
   return acc;
 }
@@ -268,9 +269,9 @@ __device__ __forceinline__ float steering_tan(float y, float h, float spd, int c
 // -u_a, v_a, u_a, -v_a, -u_b, v_b, u_b, -v_b, the opposite ones by exact negation.
 __device__ __forceinline__ void rect_interval(float x, float y, float c, float s, float nx,
                                               float ny, float& mn, float& mx) {
-  const float p = x * nx + y * ny;
-  const float r = (VEH_LENGTH / 2.0f) * hm_absf(c * nx + s * ny) +
-                  (VEH_WIDTH / 2.0f) * hm_absf(c * ny - s * nx);
+  const float p = hm_fma(x, nx, y * ny);
+  const float r = hm_fma(VEH_LENGTH / 2.0f, hm_absf(hm_fma(c, nx, s * ny)),
+                         (VEH_WIDTH / 2.0f) * hm_absf(hm_fma(c, ny, -(s * nx))));
   mn = p - r;
   mx = p + r;
 }
@@ -302,8 +303,8 @@ __device__ __forceinline__ void sat_collide(bool active, float xa, float ya, flo
       nyk[k] = k ? c : -s;
       rect_interval(xa, ya, ca, sa, nxk[k], nyk[k], pa0[k], pa1[k]);
       rect_interval(xb, yb, cb, sb, nxk[k], nyk[k], pb0[k], pb1[k]);
-      vpk[k] = nxk[k] * ddx + nyk[k] * ddy;
-      cdk[k] = cdx * nxk[k] + cdy * nyk[k];
+      vpk[k] = hm_fma(nxk[k], ddx, nyk[k] * ddy);
+      cdk[k] = hm_fma(cdx, nxk[k], cdy * nyk[k]);
       min_a = pa0[k], max_a = pa1[k], min_b = pb0[k], max_b = pb1[k];
       vp = vpk[k], cd = cdk[k], sx = nxk[k], sy = nyk[k];
     } else {  // the opposite edge: n -> -n
@@ -395,6 +396,12 @@ __device__ void reset_wave(const hwy_config& C, int lane, uint64_t seed, Veh& v)
   }
 }
 
+// road-order position of every vehicle after a reset: create_random places each car ahead of all
+// previous ones (x strictly increasing with the index), so the order is the index order
+__device__ __forceinline__ int reset_order_pos(int lane, int V) {
+  return lane < V ? lane : V + (WAVE - 1 - lane);
+}
+
 // ------------------------------------------------------------------------- observation
 __device__ __forceinline__ float feature_value(int fid, float x, float y, float spd, float h,
                                                float c, float s) {
@@ -470,7 +477,7 @@ __device__ void observe_wave(const hwy_config& C, int lane, const Veh& v, int st
   // Road.close_objects_to(ego, PERCEPTION_DISTANCE, count=N-1, see_behind, sort)
   float dx = v.x - ex, dy = v.y - ey;
   bool elig = v.present && lane >= 1 && lane < V &&
-              (__builtin_sqrtf(dx * dx + dy * dy) < PERCEPTION_DISTANCE) &&
+              (__builtin_sqrtf(hm_fma(dx, dx, dy * dy)) < PERCEPTION_DISTANCE) &&
               (C.see_behind || -2.0f * VEH_LENGTH < v.x - ex);
   const uint64_t em = ballot(elig);
   int rank;
@@ -544,7 +551,7 @@ __device__ void observe_wave(const hwy_config& C, int lane, const Veh& v, int st
 
 // ------------------------------------------------------------------------- state I/O
 __device__ __forceinline__ void load_veh(const uint32_t* st, size_t fstride, uint32_t idx, int lane,
-                                         int V, Veh& v) {
+                                         int V, Veh& v, int& order_pos) {
   v.x = hm_bits2f((st + HWY_F_X * fstride)[idx]);
   v.y = hm_bits2f((st + HWY_F_Y * fstride)[idx]);
   v.h = hm_bits2f((st + HWY_F_HEADING * fstride)[idx]);
@@ -560,12 +567,13 @@ __device__ __forceinline__ void load_veh(const uint32_t* st, size_t fstride, uin
   v.crashed = (fl & HWY_FLAG_CRASHED) != 0u;
   v.imp = (fl & HWY_FLAG_IMPACT) != 0u;
   v.present = ((fl & HWY_FLAG_PRESENT) != 0u) && lane < V;
+  order_pos = (int)((fl & HWY_FLAG_ORDER_MASK) >> HWY_FLAG_ORDER_SHIFT);
   v.aacc = 0.0f;
   v.asteer = 0.0f;
 }
 
 __device__ __forceinline__ void store_veh(uint32_t* st, size_t fstride, uint32_t idx, int lane, int V,
-                                          const Veh& v) {
+                                          const Veh& v, int order_pos) {
   // opaque copy of the offset: the 13 field addresses are rebuilt here instead of being kept
   // live (26 VGPRs) from load_veh across the whole step
   asm volatile("" : "+v"(idx));
@@ -583,7 +591,8 @@ __device__ __forceinline__ void store_veh(uint32_t* st, size_t fstride, uint32_t
   (st + HWY_F_TLANE * fstride)[idx] = live ? (uint32_t)v.tl : 0u;
   (st + HWY_F_FLAGS * fstride)[idx] =
       live ? ((v.crashed ? HWY_FLAG_CRASHED : 0u) | (v.imp ? HWY_FLAG_IMPACT : 0u) |
-              (v.present ? HWY_FLAG_PRESENT : 0u))
+              (v.present ? HWY_FLAG_PRESENT : 0u) |
+              ((uint32_t)order_pos << HWY_FLAG_ORDER_SHIFT))
            : 0u;
 }
 
@@ -940,22 +949,22 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
     // beta = atan(tan(steering) / 2) in closed form (oracle vehicle_step): cos and sin of beta
     // from u = tan(beta), cos / sin of h + beta by angle addition from the carried cos / sin h
     const float u = 0.5f * ((lane == 0 && !v.crashed) ? tan_ego : v.asteer);
-    const float cb = 1.0f / __builtin_sqrtf(1.0f + u * u);
+    const float cb = 1.0f / __builtin_sqrtf(hm_fma(u, u, 1.0f));
     const float sb = u * cb;
-    const float cdir = ch * cb - sh * sb;
-    const float sdir = sh * cb + ch * sb;
+    const float cdir = hm_fma(ch, cb, -(sh * sb));
+    const float sdir = hm_fma(sh, cb, ch * sb);
     const float vx = v.spd * cdir;
     const float vy = v.spd * sdir;
-    v.x = v.x + vx * dt;
-    v.y = v.y + vy * dt;
+    v.x = hm_fma(vx, dt, v.x);
+    v.y = hm_fma(vy, dt, v.y);
     if (v.imp) {
       v.x = v.x + v.ix;
       v.y = v.y + v.iy;
       v.crashed = true;
       v.imp = false;
     }
-    v.h = v.h + v.spd * sb / (VEH_LENGTH / 2.0f) * dt;
-    v.spd = v.spd + v.aacc * dt;
+    v.h = hm_fma(v.spd * sb, dt * (2.0f / VEH_LENGTH), v.h);  // speed sin(beta) / (L/2) dt
+    v.spd = hm_fma(v.aacc, dt, v.spd);
     v.ln = closest_lane(v.y, lanes);  // on_state_update
   }
 
@@ -1026,7 +1035,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
                 vb = shf(v.spd, b);
     // exact pre-check (are_polygons_intersecting is only called inside it), then the SAT test
     const float dx = xb - xa, dy = yb - ya;
-    const bool pass = has && !(__builtin_sqrtf(dx * dx + dy * dy) >
+    const bool pass = has && !(__builtin_sqrtf(hm_fma(dx, dx, dy * dy)) >
                                (VEH_DIAGONAL + VEH_DIAGONAL) / 2.0f + va * dt);
     if (!wave_any(pass)) continue;
     bool inter, will;
@@ -1076,7 +1085,8 @@ __global__ void __launch_bounds__(256, 4) hwy_step_kernel(StepParams P) {
   WAVE_T(e, lane, 0, __builtin_amdgcn_s_memtime());
   WAVE_T(e, lane, 3, __builtin_amdgcn_s_memrealtime());
   Veh v;
-  load_veh(st, fstride, idx, lane, V, v);
+  int order_pos;
+  load_veh(st, fstride, idx, lane, V, v, order_pos);
   const uint32_t ew = (st + HWY_F_ENV * fstride)[idx];
   int step = rdli((int)ew, HWY_E_STEP);
   int episode = rdli((int)ew, HWY_E_EPISODE);
@@ -1091,10 +1101,14 @@ __global__ void __launch_bounds__(256, 4) hwy_step_kernel(StepParams P) {
   const float dt = 1.0f / (float)C.sim_freq;
   const int frames = C.sim_freq / C.policy_freq;
   const float a0 = P.actions[2 * (size_t)e], a1 = P.actions[2 * (size_t)e + 1];
+  // the road order of the stored positions, kept from the previous step (flags bits 8-13; the
+  // absent lanes follow the present ones by descending index), validated -- and repaired or
+  // rebuilt when the state was written by someone else -- before frame 0 uses it
   RoadOrder ro;
-  ro.rk = lane;
-  ro.ord = lane;
-  ro.valid = false;
+  ro.rk = lane < V ? order_pos : V + (WAVE - 1 - lane);
+  ro.ord = __builtin_amdgcn_ds_permute(ro.rk << 2, lane);
+  ro.valid = true;
+  road_order(lane, v, ballot(v.present), ro);
   float cos_h, sin_h;
   hm_sincosf(v.h, &sin_h, &cos_h);
   SEC(sp, 15);
@@ -1151,12 +1165,13 @@ __global__ void __launch_bounds__(256, 4) hwy_step_kernel(StepParams P) {
     reset_wave(C, lane, seed, v);
     step = 0;
     ep_return = 0.0f;
+    ro.rk = reset_order_pos(lane, V);
   }
   SEC(sp, 12);
   observe_wave(C, lane, v, step, seed, P.pe_table, P.obs + (size_t)e * C.obs_vehicles * P.fout,
                P.fout, lds_vor[w], lds_inv[w]);
   SEC(sp, 13);
-  store_veh(st, fstride, idx, lane, V, v);
+  store_veh(st, fstride, idx, lane, V, v, ro.rk);
   store_env_words(st, fstride, idx, lane, step, episode, seed, rdlf(v.aacc, 0), rdlf(v.asteer, 0),
                   ep_return);
   SEC(sp, 14);
@@ -1184,7 +1199,7 @@ __global__ void __launch_bounds__(256) hwy_reset_kernel(StepParams P) {
   if (P.obs)
     observe_wave(C, lane, v, 0, seed, P.pe_table, P.obs + (size_t)e * C.obs_vehicles * P.fout,
                  P.fout, lds_vor[w], lds_inv[w]);
-  store_veh(P.state, fstride, idx, lane, V, v);
+  store_veh(P.state, fstride, idx, lane, V, v, reset_order_pos(lane, V));
   store_env_words(P.state, fstride, idx, lane, 0, 0, seed, 0.0f, 0.0f, 0.0f);
 }
 

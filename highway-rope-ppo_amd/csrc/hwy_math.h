@@ -4,8 +4,10 @@
  * Why: the highway step is chaotic (MOBIL thresholds, collision tests), so GPU/CPU parity is
  * only meaningful if both sides round identically. libm (glibc) and the device library (ocml)
  * differ in the last ulp of sin/atan/pow, so both sides use these routines instead. They use
- * only IEEE-754 correctly rounded operations (+ - * / sqrt, floor, int<->float), so with
- * -ffp-contract=off they produce the same bits on x86-64 (SSE) and on gfx950.
+ * only IEEE-754 correctly rounded operations (+ - * / sqrt, fma, floor, int<->float), so with
+ * -ffp-contract=off they produce the same bits on x86-64 (SSE) and on gfx950.  Fused
+ * multiply-adds are explicit (hm_fma: v_fma_f32 on gfx950, the correctly rounded fmaf on the
+ * host), never left to the compiler's contraction, so both sides fuse the same operations.
  * Polynomials are the classic Cephes single-precision ones (S. Moshier, public domain),
  * accurate to ~1-3 ulp on the ranges used; tests/test_math.py checks them against libm double.
  *
@@ -39,6 +41,8 @@ HWY_HD uint32_t hm_f2bits(float f) {
 }
 
 HWY_HD float hm_absf(float x) { return hm_bits2f(hm_f2bits(x) & 0x7fffffffu); }
+/* a * b + c with one rounding (IEEE fusedMultiplyAdd) */
+HWY_HD float hm_fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 HWY_HD int hm_isnan(float x) { return x != x; }
 
 /* numpy.clip semantics for scalars: NaN propagates. */
@@ -112,23 +116,17 @@ HWY_HD float hm_sincos_core(float xx, int want_cos) {
     j -= 4u;
   }
   if (want_cos && j > 1u) sign = -sign;
-  x = ((x - y * DP1) - y * DP2) - y * DP3;
+  x = hm_fma(-y, DP3, hm_fma(-y, DP2, hm_fma(-y, DP1, x)));
   float z = x * x;
   int use_cos_poly = want_cos ? !(j == 1u || j == 2u) : (j == 1u || j == 2u);
   float r;
   if (use_cos_poly) {
-    r = 2.443315711809948E-005f;
-    r = r * z - 1.388731625493765E-003f;
-    r = r * z + 4.166664568298827E-002f;
-    r = r * (z * z);
-    r = r - 0.5f * z;
-    r = r + 1.0f;
+    r = hm_fma(hm_fma(2.443315711809948E-005f, z, -1.388731625493765E-003f), z,
+               4.166664568298827E-002f);
+    r = hm_fma(r, z * z, hm_fma(-0.5f, z, 1.0f));
   } else {
-    r = -1.9515295891E-4f;
-    r = r * z + 8.3321608736E-3f;
-    r = r * z - 1.6666654611E-1f;
-    r = r * (z * x);
-    r = r + x;
+    r = hm_fma(hm_fma(-1.9515295891E-4f, z, 8.3321608736E-3f), z, -1.6666654611E-1f);
+    r = hm_fma(r, z * x, x);
   }
   return sign < 0 ? -r : r;
 }
@@ -167,19 +165,13 @@ HWY_HD void hm_sincosf(float xx, float* s_out, float* c_out) {
     j -= 4u;
   }
   if (j > 1u) sign_c = -sign_c;
-  x = ((x - y * DP1) - y * DP2) - y * DP3;
+  x = hm_fma(-y, DP3, hm_fma(-y, DP2, hm_fma(-y, DP1, x)));
   const float z = x * x;
-  float rc = 2.443315711809948E-005f;
-  rc = rc * z - 1.388731625493765E-003f;
-  rc = rc * z + 4.166664568298827E-002f;
-  rc = rc * (z * z);
-  rc = rc - 0.5f * z;
-  rc = rc + 1.0f;
-  float rs = -1.9515295891E-4f;
-  rs = rs * z + 8.3321608736E-3f;
-  rs = rs * z - 1.6666654611E-1f;
-  rs = rs * (z * x);
-  rs = rs + x;
+  float rc = hm_fma(hm_fma(2.443315711809948E-005f, z, -1.388731625493765E-003f), z,
+                    4.166664568298827E-002f);
+  rc = hm_fma(rc, z * z, hm_fma(-0.5f, z, 1.0f));
+  float rs = hm_fma(hm_fma(-1.9515295891E-4f, z, 8.3321608736E-3f), z, -1.6666654611E-1f);
+  rs = hm_fma(rs, z * x, x);
   const int swap = (j == 1u || j == 2u);
   const float s = swap ? rc : rs, c = swap ? rs : rc;
   *s_out = sign_s < 0 ? -s : s;
@@ -209,11 +201,9 @@ HWY_HD float hm_atanf(float xx) {
     y = 0.0f;
   }
   float z = x * x;
-  float p = 8.05374449538e-2f;
-  p = p * z - 1.38776856032E-1f;
-  p = p * z + 1.99777106478E-1f;
-  p = p * z - 3.33329491539E-1f;
-  y = y + (p * z * x + x);
+  float p = hm_fma(hm_fma(hm_fma(8.05374449538e-2f, z, -1.38776856032E-1f), z,
+                          1.99777106478E-1f), z, -3.33329491539E-1f);
+  y = y + hm_fma(p * z, x, x);
   return sign < 0 ? -y : y;
 }
 
@@ -241,12 +231,10 @@ HWY_HD float hm_asinf(float xx) {
       z = x * x;
       flag = 0;
     }
-    float p = 4.2163199048E-2f;
-    p = p * z + 2.4181311049E-2f;
-    p = p * z + 4.5470025998E-2f;
-    p = p * z + 7.4953002686E-2f;
-    p = p * z + 1.6666752422E-1f;
-    z = p * z * x + x;
+    float p = hm_fma(hm_fma(hm_fma(hm_fma(4.2163199048E-2f, z, 2.4181311049E-2f), z,
+                                      4.5470025998E-2f), z, 7.4953002686E-2f), z,
+                     1.6666752422E-1f);
+    z = hm_fma(p * z, x, x);
     if (flag) {
       z = z + z;
       z = HM_PIO2_F - z;
@@ -261,18 +249,15 @@ HWY_HD float hm_expf(float xx) {
   if (hm_isnan(x)) return x;
   if (x > 88.72283905206835f) return hm_bits2f(0x7f800000u);
   if (x < -103.278929903431851103f) return 0.0f;
-  float z = hm_floorf(1.44269504088896341f * x + 0.5f);
-  x = x - z * 0.693359375f;
-  x = x - z * -2.12194440e-4f;
+  float z = hm_floorf(hm_fma(1.44269504088896341f, x, 0.5f));
+  x = hm_fma(-z, 0.693359375f, x);
+  x = hm_fma(z, 2.12194440e-4f, x);
   int n = (int)z;
   z = x * x;
-  float p = 1.9875691500E-4f;
-  p = p * x + 1.3981999507E-3f;
-  p = p * x + 8.3334519073E-3f;
-  p = p * x + 4.1665795894E-2f;
-  p = p * x + 1.6666665459E-1f;
-  p = p * x + 5.0000001201E-1f;
-  p = p * z + x + 1.0f;
+  float p = hm_fma(hm_fma(1.9875691500E-4f, x, 1.3981999507E-3f), x, 8.3334519073E-3f);
+  p = hm_fma(hm_fma(hm_fma(p, x, 4.1665795894E-2f), x, 1.6666665459E-1f), x,
+             5.0000001201E-1f);
+  p = hm_fma(p, z, x) + 1.0f;
   return hm_ldexpf(p, n);
 }
 
@@ -291,21 +276,16 @@ HWY_HD float hm_logf(float xx) {
     x = x - 1.0f;
   }
   float z = x * x;
-  float y = 7.0376836292E-2f;
-  y = y * x - 1.1514610310E-1f;
-  y = y * x + 1.1676998740E-1f;
-  y = y * x - 1.2420140846E-1f;
-  y = y * x + 1.4249322787E-1f;
-  y = y * x - 1.6668057665E-1f;
-  y = y * x + 2.0000714765E-1f;
-  y = y * x - 2.4999993993E-1f;
-  y = y * x + 3.3333331174E-1f;
+  float y = hm_fma(hm_fma(hm_fma(7.0376836292E-2f, x, -1.1514610310E-1f), x, 1.1676998740E-1f),
+                   x, -1.2420140846E-1f);
+  y = hm_fma(hm_fma(hm_fma(y, x, 1.4249322787E-1f), x, -1.6668057665E-1f), x, 2.0000714765E-1f);
+  y = hm_fma(hm_fma(y, x, -2.4999993993E-1f), x, 3.3333331174E-1f);
   y = y * x * z;
   float fe = (float)e;
-  if (e) y = y + -2.12194440e-4f * fe;
-  y = y + -0.5f * z;
+  if (e) y = hm_fma(-2.12194440e-4f, fe, y);
+  y = hm_fma(-0.5f, z, y);
   z = x + y;
-  if (e) z = z + 0.693359375f * fe;
+  if (e) z = hm_fma(0.693359375f, fe, z);
   return z;
 }
 
@@ -320,7 +300,7 @@ HWY_HD float hm_powf(float b, float p) {
 HWY_HD float hm_wrap_to_pi(float x) {
   float t = x + HM_PI_F;
   float n = hm_floorf(t / HM_TWO_PI_F);
-  float r = t - n * HM_TWO_PI_F;
+  float r = hm_fma(-n, HM_TWO_PI_F, t);
   if (r < 0.0f) r = r + HM_TWO_PI_F;
   if (r >= HM_TWO_PI_F) r = r - HM_TWO_PI_F;
   return r - HM_PI_F;

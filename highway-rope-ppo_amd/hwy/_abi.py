@@ -38,6 +38,7 @@ F_LANE, F_TLANE, F_FLAGS, F_ENV = 9, 10, 11, 12
 NFIELDS = 13
 E_STEP, E_EPISODE, E_SEED_LO, E_SEED_HI, E_EGO_ACC, E_EGO_STEER, E_RETURN = range(7)
 FLAG_CRASHED, FLAG_IMPACT, FLAG_PRESENT = 1, 2, 4
+FLAG_ORDER_SHIFT = 8  # bits 8-13: road-order position (include/hwy.h)
 FLOAT_FIELDS = (F_X, F_Y, F_HEADING, F_SPEED, F_TSPEED, F_DELTA, F_TIMER, F_IMPX, F_IMPY)
 
 # Episode horizon in policy steps.  highway-env 1.10.1 truncates on env.time >= duration; the

@@ -132,7 +132,9 @@ enum hwy_field {
   HWY_F_IMPX, HWY_F_IMPY, /* pending collision impact */
   HWY_F_LANE,    /* int: closest lane id */
   HWY_F_TLANE,   /* int: target lane id */
-  HWY_F_FLAGS,   /* int: bit0 crashed, bit1 impact pending, bit2 present */
+  HWY_F_FLAGS,   /* int: bit0 crashed, bit1 impact pending, bit2 present, bits 8-13 the
+                    vehicle's position in the road order (x ascending, index descending) of the
+                    stored positions -- a hint the step validates before use */
   HWY_F_ENV,     /* per-env words, see enum hwy_env_word */
   HWY_NFIELDS
 };
@@ -147,6 +149,8 @@ enum hwy_env_word {
 #define HWY_FLAG_CRASHED 1u
 #define HWY_FLAG_IMPACT 2u
 #define HWY_FLAG_PRESENT 4u
+#define HWY_FLAG_ORDER_SHIFT 8u
+#define HWY_FLAG_ORDER_MASK (63u << HWY_FLAG_ORDER_SHIFT)
 
 int hwy_abi_version(void);
 /* sizeof(hwy_config) as compiled into the library (binding layout check). */

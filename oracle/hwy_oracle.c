@@ -54,6 +54,7 @@
 #define LANE_CHANGE_DELAY 1.0f
 #define PERCEPTION_DISTANCE 200.0f /* 5 * Vehicle.MAX_SPEED */
 #define TWO_SQRT_AB 7.745966692414834f /* 2 * sqrt(-COMFORT_ACC_MAX * COMFORT_ACC_MIN) */
+#define INV_TWO_SQRT_AB 0.12909944487358056f /* 1 / TWO_SQRT_AB, correctly rounded */
 #define VEH_DIAGONAL 5.385164807134504f /* sqrt(LENGTH^2 + WIDTH^2) */
 
 typedef struct {
@@ -116,6 +117,29 @@ static void load_road(Road* r, const hwy_config* cfg, uint32_t* st, int E, int e
   r->ep_return = hm_bits2f(ew[HWY_E_RETURN]);
 }
 
+/* Position of vehicle i in the road order of the current positions, as the kernel keeps it in
+ * the flags word (include/hwy.h): present vehicles by (x ascending with -0 == +0, then index
+ * descending), every absent lane after them by descending index. */
+static uint64_t road_key(float x, int i) {
+  uint32_t u = hm_f2bits(x + 0.0f);
+  uint32_t s = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((uint64_t)s << 32) | (uint32_t)(HWY_MAX_VEHICLES - 1 - i);
+}
+static int road_order_pos(const Road* r, int i) {
+  int npres = 0;
+  for (int k = 0; k < r->V; ++k) npres += r->v[k].present ? 1 : 0;
+  if (!r->v[i].present) {
+    int above = 0;
+    for (int k = i + 1; k < HWY_MAX_VEHICLES; ++k) above += (k >= r->V || !r->v[k].present) ? 1 : 0;
+    return npres + above;
+  }
+  const uint64_t key = road_key(r->v[i].x, i);
+  int pos = 0;
+  for (int k = 0; k < r->V; ++k)
+    if (r->v[k].present && road_key(r->v[k].x, k) < key) ++pos;
+  return pos;
+}
+
 static void store_road(const Road* r, uint32_t* st, int E, int e) {
   for (int i = 0; i < HWY_MAX_VEHICLES; ++i) {
     if (i >= r->V) {
@@ -136,7 +160,8 @@ static void store_road(const Road* r, uint32_t* st, int E, int e) {
     fld(st, HWY_F_TLANE, E, e)[i] = (uint32_t)v->target_lane;
     fld(st, HWY_F_FLAGS, E, e)[i] = (v->crashed ? HWY_FLAG_CRASHED : 0u) |
                                     (v->has_impact ? HWY_FLAG_IMPACT : 0u) |
-                                    (v->present ? HWY_FLAG_PRESENT : 0u);
+                                    (v->present ? HWY_FLAG_PRESENT : 0u) |
+                                    ((uint32_t)road_order_pos(r, i) << HWY_FLAG_ORDER_SHIFT);
   }
   uint32_t* ew = fld(st, HWY_F_ENV, E, e);
   for (int w = 0; w < HWY_MAX_VEHICLES; ++w) ew[w] = 0u;
@@ -213,8 +238,8 @@ static float desired_gap(const Road* r, int ev, int fv) {
   float cb = hm_cosf(b->heading), sb = hm_sinf(b->heading);
   float avx = a->speed * ca, avy = a->speed * sa;
   float bvx = b->speed * cb, bvy = b->speed * sb;
-  float dv = (avx - bvx) * ca + (avy - bvy) * sa;
-  return (DISTANCE_WANTED + a->speed * TIME_WANTED) + (a->speed * dv) / TWO_SQRT_AB;
+  float dv = hm_fma(avx - bvx, ca, (avy - bvy) * sa);
+  return hm_fma(a->speed, TIME_WANTED, DISTANCE_WANTED) + (a->speed * dv) * INV_TWO_SQRT_AB;
 }
 
 /* IDMVehicle.acceleration(ego_vehicle, front_vehicle) evaluated with self.DELTA of `self` */
@@ -224,11 +249,11 @@ static float idm_acceleration(const Road* r, int self, int ev, int fv) {
   float tsp = (ev == 0) ? 0.0f : e->target_speed; /* plain Vehicle has no target_speed */
   tsp = hm_clipf(tsp, 0.0f, r->cfg->speed_limit);
   float base = hm_maxf(e->speed, 0.0f) / hm_absf(hm_not_zero(tsp));
-  float acc = COMFORT_ACC_MAX * (1.0f - hm_powf(base, r->v[self].delta));
+  float acc = hm_fma(-COMFORT_ACC_MAX, hm_powf(base, r->v[self].delta), COMFORT_ACC_MAX);
   if (fv >= 0) {
     float d = lane_s(r->v[fv].x) - lane_s(e->x); /* lane_distance_to */
     float g = desired_gap(r, ev, fv) / hm_not_zero(d);
-    acc = acc - COMFORT_ACC_MAX * (g * g);
+    acc = hm_fma(-COMFORT_ACC_MAX, g * g, acc);
   }
   return acc;
 }
@@ -359,21 +384,21 @@ static void vehicle_step(Road* r, int i) {
    * angle; the traffic's comes from steering_tan.  kinematics_upstream is the transliteration. */
   float tan_delta = i == 0 ? hm_tanf(v->act_steer) : v->act_tan;
   float u = 0.5f * tan_delta;
-  float cbeta = 1.0f / sqrtf(1.0f + u * u);
+  float cbeta = 1.0f / sqrtf(hm_fma(u, u, 1.0f));
   float sbeta = u * cbeta;
   float ch = hm_cosf(v->heading), sh = hm_sinf(v->heading);
-  float vx = v->speed * (ch * cbeta - sh * sbeta);
-  float vy = v->speed * (sh * cbeta + ch * sbeta);
-  v->x = v->x + vx * dt;
-  v->y = v->y + vy * dt;
+  float vx = v->speed * hm_fma(ch, cbeta, -(sh * sbeta));
+  float vy = v->speed * hm_fma(sh, cbeta, ch * sbeta);
+  v->x = hm_fma(vx, dt, v->x);
+  v->y = hm_fma(vy, dt, v->y);
   if (v->has_impact) {
     v->x = v->x + v->imp_x;
     v->y = v->y + v->imp_y;
     v->crashed = 1;
     v->has_impact = 0;
   }
-  v->heading = v->heading + v->speed * sbeta / (VEH_LENGTH / 2.0f) * dt;
-  v->speed = v->speed + v->act_acc * dt;
+  v->heading = hm_fma(v->speed * sbeta, dt * (2.0f / VEH_LENGTH), v->heading);
+  v->speed = hm_fma(v->act_acc, dt, v->speed);
   v->lane = closest_lane(v->y, r->cfg->lanes_count); /* on_state_update */
 }
 
@@ -465,9 +490,9 @@ static void are_polygons_intersecting(float A[5][2], float B[5][2], float dax, f
  * hwyo_sat_compare / tests/test_oracle_env.py. */
 static void rect_interval(float x, float y, float c, float s, float nx, float ny, float* mn,
                           float* mx) {
-  float p = x * nx + y * ny;
-  float r = (VEH_LENGTH / 2.0f) * hm_absf(c * nx + s * ny) +
-            (VEH_WIDTH / 2.0f) * hm_absf(c * ny - s * nx);
+  float p = hm_fma(x, nx, y * ny);
+  float r = hm_fma(VEH_LENGTH / 2.0f, hm_absf(hm_fma(c, nx, s * ny)),
+                   (VEH_WIDTH / 2.0f) * hm_absf(hm_fma(c, ny, -(s * nx))));
   *mn = p - r;
   *mx = p + r;
 }
@@ -486,8 +511,8 @@ static void rect_sat(float xa, float ya, float ca, float sa, float dax, float da
     float min_a, max_a, min_b, max_b;
     rect_interval(xa, ya, ca, sa, nx, ny, &min_a, &max_a);
     rect_interval(xb, yb, cb, sb, nx, ny, &min_b, &max_b);
-    float vp = nx * ddx + ny * ddy;
-    float cd = cdx * nx + cdy * ny;
+    float vp = hm_fma(nx, ddx, ny * ddy);
+    float cd = hm_fma(cdx, nx, cdy * ny);
     float sx = nx, sy = ny;
     if (e & 2) { /* the opposite edge: n -> -n */
       float t = min_a;
@@ -540,12 +565,12 @@ static void kin_upstream(float h, float spd, float delta, float* vx, float* vy, 
 }
 static void kin_closed(float h, float spd, float tan_delta, float* vx, float* vy, float* hr) {
   float u = 0.5f * tan_delta;
-  float cbeta = 1.0f / sqrtf(1.0f + u * u);
+  float cbeta = 1.0f / sqrtf(hm_fma(u, u, 1.0f));
   float sbeta = u * cbeta;
   float ch = hm_cosf(h), sh = hm_sinf(h);
-  *vx = spd * (ch * cbeta - sh * sbeta);
-  *vy = spd * (sh * cbeta + ch * sbeta);
-  *hr = spd * sbeta / (VEH_LENGTH / 2.0f);
+  *vx = spd * hm_fma(ch, cbeta, -(sh * sbeta));
+  *vy = spd * hm_fma(sh, cbeta, ch * sbeta);
+  *hr = (spd * sbeta) * (2.0f / VEH_LENGTH);
 }
 int hwyo_kin_compare(const float* in, int n, float* out) {
   for (int i = 0; i < n; ++i) {
@@ -594,7 +619,7 @@ static void handle_collisions(Road* r, int i, int j) {
   Veh* b = &r->v[j];
   float dt = r->dt;
   float dx = b->x - a->x, dy = b->y - a->y;
-  if (sqrtf(dx * dx + dy * dy) > (VEH_DIAGONAL + VEH_DIAGONAL) / 2.0f + a->speed * dt) return;
+  if (sqrtf(hm_fma(dx, dx, dy * dy)) > (VEH_DIAGONAL + VEH_DIAGONAL) / 2.0f + a->speed * dt) return;
   const float ca = hm_cosf(a->heading), sa = hm_sinf(a->heading);
   const float cb = hm_cosf(b->heading), sb = hm_sinf(b->heading);
   float dax = (a->speed * ca) * dt, day = (a->speed * sa) * dt;
@@ -693,7 +718,7 @@ static void observe(const Road* r, float* obs, const float* pe_table) {
     const Veh* v = &r->v[k];
     if (k == 0 || !v->present) continue;
     float dx = v->x - ego->x, dy = v->y - ego->y;
-    if (!(sqrtf(dx * dx + dy * dy) < PERCEPTION_DISTANCE)) continue;
+    if (!(sqrtf(hm_fma(dx, dx, dy * dy)) < PERCEPTION_DISTANCE)) continue;
     if (!(cfg->see_behind || -2.0f * VEH_LENGTH < lane_s(v->x) - lane_s(ego->x))) continue;
     close[nclose++] = k;
   }
