@@ -253,12 +253,12 @@ __device__ __forceinline__ float steering_tan(float y, float h, float spd, int c
   float lat = lane_lat(y, c);
   float lane_future_heading = 0.0f;
   float lateral_speed_command = -KP_LATERAL * lat;
-  float heading_command =
-      hm_asinf(hm_clipf(lateral_speed_command / hm_not_zero(spd), -1.0f, 1.0f));
+  const float inv_spd = 1.0f / hm_not_zero(spd);  // both of upstream's divisions by not_zero(speed)
+  float heading_command = hm_asinf(hm_clipf(lateral_speed_command * inv_spd, -1.0f, 1.0f));
   float heading_ref = lane_future_heading + hm_clipf(heading_command, -HM_PIO4_F, HM_PIO4_F);
   float heading_rate_command = KP_HEADING * hm_wrap_to_pi(heading_ref - h);
   const float z =
-      hm_clipf((VEH_LENGTH / 2.0f) / hm_not_zero(spd) * heading_rate_command, -1.0f, 1.0f);
+      hm_clipf(((VEH_LENGTH / 2.0f) * inv_spd) * heading_rate_command, -1.0f, 1.0f);
   const float t = 2.0f * (z / __builtin_sqrtf((1.0f - z) * (1.0f + z)));
   return hm_clipf(t, -TAN_MAX_STEERING, TAN_MAX_STEERING);
 }
@@ -466,12 +466,12 @@ __device__ __forceinline__ void write_pe_row(const float* vals, int F, int kind,
 }
 
 // KinematicObservation.observe + fused wrapper for the env of this wave.
-__device__ void observe_wave(const hwy_config& C, int lane, const Veh& v, int step, uint64_t seed,
-                             const float* pe_table, float* obs_env, int fout, int* lds_vor,
-                             int* lds_inv) {
+// ch / sh: hm_cosf / hm_sinf of v.h (the step carries them from the last frame)
+__device__ void observe_wave(const hwy_config& C, int lane, const Veh& v, float ch, float sh,
+                             int step, uint64_t seed, const float* pe_table, float* obs_env,
+                             int fout, int* lds_vor, int* lds_inv) {
   const int V = C.vehicles_count + 1;
   const int N = C.obs_vehicles, F = C.n_features;
-  const float ch = hm_cosf(v.h), sh = hm_sinf(v.h);
   const float ex = rdlf(v.x, 0), ey = rdlf(v.y, 0), eh = rdlf(v.h, 0), espd = rdlf(v.spd, 0);
   const float ec = rdlf(ch, 0), es = rdlf(sh, 0);
   // Road.close_objects_to(ego, PERCEPTION_DISTANCE, count=N-1, see_behind, sort)
@@ -1127,7 +1127,7 @@ __global__ void __launch_bounds__(256, 4) hwy_step_kernel(StepParams P) {
   float rew = 0.0f;
   int terminated = 0;
   if (lane == 0) {
-    const float forward_speed = v.spd * hm_cosf(v.h);
+    const float forward_speed = v.spd * cos_h;  // hm_cosf(v.h), carried from the last frame
     const float scaled_speed = hm_lmap(forward_speed, C.reward_speed_range[0],
                                        C.reward_speed_range[1], 0.0f, 1.0f);
     const float collision = v.crashed ? 1.0f : 0.0f;
@@ -1166,10 +1166,12 @@ __global__ void __launch_bounds__(256, 4) hwy_step_kernel(StepParams P) {
     step = 0;
     ep_return = 0.0f;
     ro.rk = reset_order_pos(lane, V);
+    cos_h = 1.0f;  // hm_cosf / hm_sinf of the reset heading 0, exactly
+    sin_h = 0.0f;
   }
   SEC(sp, 12);
-  observe_wave(C, lane, v, step, seed, P.pe_table, P.obs + (size_t)e * C.obs_vehicles * P.fout,
-               P.fout, lds_vor[w], lds_inv[w]);
+  observe_wave(C, lane, v, cos_h, sin_h, step, seed, P.pe_table,
+               P.obs + (size_t)e * C.obs_vehicles * P.fout, P.fout, lds_vor[w], lds_inv[w]);
   SEC(sp, 13);
   store_veh(st, fstride, idx, lane, V, v, ro.rk);
   store_env_words(st, fstride, idx, lane, step, episode, seed, rdlf(v.aacc, 0), rdlf(v.asteer, 0),
@@ -1197,8 +1199,8 @@ __global__ void __launch_bounds__(256) hwy_reset_kernel(StepParams P) {
   Veh v;
   reset_wave(C, lane, seed, v);
   if (P.obs)
-    observe_wave(C, lane, v, 0, seed, P.pe_table, P.obs + (size_t)e * C.obs_vehicles * P.fout,
-                 P.fout, lds_vor[w], lds_inv[w]);
+    observe_wave(C, lane, v, 1.0f, 0.0f, 0, seed, P.pe_table,
+                 P.obs + (size_t)e * C.obs_vehicles * P.fout, P.fout, lds_vor[w], lds_inv[w]);
   store_veh(P.state, fstride, idx, lane, V, v, reset_order_pos(lane, V));
   store_env_words(P.state, fstride, idx, lane, 0, 0, seed, 0.0f, 0.0f, 0.0f);
 }

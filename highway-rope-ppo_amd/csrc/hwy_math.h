@@ -296,10 +296,12 @@ HWY_HD float hm_powf(float b, float p) {
   return hm_expf(p * hm_logf(b));
 }
 
-/* utils.wrap_to_pi: ((x + pi) % (2 pi)) - pi with Python's floored modulo. */
+/* utils.wrap_to_pi: ((x + pi) % (2 pi)) - pi with Python's floored modulo.  The quotient is
+ * taken with the reciprocal (a possible off-by-one next to a multiple of 2 pi is corrected
+ * below). */
 HWY_HD float hm_wrap_to_pi(float x) {
   float t = x + HM_PI_F;
-  float n = hm_floorf(t / HM_TWO_PI_F);
+  float n = hm_floorf(t * 0.15915494309189535f);
   float r = hm_fma(-n, HM_TWO_PI_F, t);
   if (r < 0.0f) r = r + HM_TWO_PI_F;
   if (r >= HM_TWO_PI_F) r = r - HM_TWO_PI_F;

@@ -358,9 +358,12 @@ __host__ __device__ inline TileGeom tile_geom(int S, int H, int sb, int hb) {
   return T;
 }
 // ring depth of the row kernels for H (ppo_rows<H/64, NW>: 16-column tiles per wave TW)
+#ifndef HWY_RING_D2
+#define HWY_RING_D2 4  // weight blocks in flight per wave when a wave owns <= 2 column tiles
+#endif
 __host__ __device__ inline int rows_ring_depth(int H) {
   const int qh = H / 64, nw = (qh % 2 == 0) ? 8 : 4, tw = H / nw / 16;
-  return tw <= 4 ? 4 : 2;
+  return tw <= 2 ? HWY_RING_D2 : (tw <= 4 ? 4 : 2);
 }
 __host__ __device__ inline void rows_blocks(int S, int H, int* sb, int* hb) {
   const int D = rows_ring_depth(H);
@@ -763,7 +766,7 @@ __device__ __forceinline__ void zero_acc(f32x4 (&acc)[TW]) {
 }
 
 template <int TW>
-constexpr int ring_depth() { return TW <= 2 ? 4 : (TW <= 4 ? 4 : 2); }
+constexpr int ring_depth() { return TW <= 2 ? HWY_RING_D2 : (TW <= 4 ? 4 : 2); }
 
 // segment table of the row kernels: forward W1, W2, Wa1, Wc1 ([N][K]); backward Wa1, Wc1, W2
 // read k-major for dh2 = dac [Wa1; Wc1] and dh1 = dh2 W2.  With a tile image (TileGeom; kept by

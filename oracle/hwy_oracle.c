@@ -335,10 +335,11 @@ static float steering_tan_v(const Veh* me, int c) {
   float lat = lane_lat(me->y, c);
   float lane_future_heading = 0.0f;
   float lateral_speed_command = -KP_LATERAL * lat;
-  float heading_command = hm_asinf(hm_clipf(lateral_speed_command / hm_not_zero(me->speed), -1.0f, 1.0f));
+  float inv_spd = 1.0f / hm_not_zero(me->speed); /* both divisions by not_zero(speed) */
+  float heading_command = hm_asinf(hm_clipf(lateral_speed_command * inv_spd, -1.0f, 1.0f));
   float heading_ref = lane_future_heading + hm_clipf(heading_command, -HM_PIO4_F, HM_PIO4_F);
   float heading_rate_command = KP_HEADING * hm_wrap_to_pi(heading_ref - me->heading);
-  float z = hm_clipf((VEH_LENGTH / 2.0f) / hm_not_zero(me->speed) * heading_rate_command, -1.0f, 1.0f);
+  float z = hm_clipf(((VEH_LENGTH / 2.0f) * inv_spd) * heading_rate_command, -1.0f, 1.0f);
   float t = 2.0f * (z / sqrtf((1.0f - z) * (1.0f + z)));
   return hm_clipf(t, -TAN_MAX_STEERING, TAN_MAX_STEERING);
 }

@@ -233,11 +233,13 @@ def test_closed_form_steering_and_kinematics_match_upstream_forms():
     # tangents come from cancelling heading differences: absolute floor)
     tol = 2e-6 + 2e-5 * np.abs(t64)
     assert np.all(np.abs(t_cf - t64) <= tol)
-    # the binary32 angle form agrees with it, except where the slip command saturates (|z| = 1):
-    # tan(float(pi/2)) is negative in binary32, which flips that steering to the opposite clip
-    bad = np.abs(t_up - t_cf) > 1e-6 + 2e-6 * np.abs(t_cf)
+    # the binary32 angle form follows float64 as closely, except where the slip command
+    # saturates (|z| = 1): tan(float(pi/2)) is negative in binary32, which flips that steering
+    # to the opposite clip
+    bad = np.sign(t_up) != np.sign(t_cf)
     assert np.all(np.abs(t_up[bad] + t64[bad]) <= 1e-5 * np.abs(t64[bad]))
     assert np.all(np.abs(np.abs(t64[bad]) - np.sqrt(3.0)) < 1e-5)
+    assert np.all(np.abs(t_up[~bad] - t64[~bad]) <= tol[~bad])
     # kinematics (vx, vy, heading rate), closed form vs angle form, for the ego angle and for the
     # traffic steering where both steering forms agree
     scale = np.abs(p[:, 2:3]).astype(np.float64) + 1e-3
