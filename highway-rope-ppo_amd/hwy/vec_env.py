@@ -63,6 +63,9 @@ class HighwayVecEnv:
 
     # ------------------------------------------------------------------ setup
     def _create(self):
+        # bumped whenever a launch argument a captured rollout graph bakes in changes (handle,
+        # seed schedule, PE table): ppo/rollout.py re-captures then
+        self.launch_version = getattr(self, "launch_version", 0) + 1
         with torch.cuda.device(self.device):
             h = ctypes.c_void_p()
             check(lib().hwy_create(ctypes.byref(self._cfg), self.device.index, ctypes.byref(h)),
@@ -138,6 +141,7 @@ class HighwayVecEnv:
         check(lib().hwy_set_pe_table(self._handle, t.ctypes.data_as(ctypes.c_void_p), int(t.size)),
               "hwy_set_pe_table")
         self._pe_table = t
+        self.launch_version += 1
 
     # ------------------------------------------------------------------ API
     def reset(self, *, seed: Optional[int] = None, options: Optional[dict] = None,
@@ -194,6 +198,7 @@ class HighwayVecEnv:
             c.seed_stride = int(seed_stride)
         check(lib().hwy_set_seed_schedule(self._handle, c.seed_base, c.env_offset, c.seed_stride),
               "hwy_set_seed_schedule")
+        self.launch_version += 1
 
     def export_state(self) -> torch.Tensor:
         out = torch.empty(NFIELDS, self.num_envs, HWY_MAX_VEHICLES, dtype=torch.int32,

@@ -310,6 +310,7 @@ def _train_vector(env, agent, max_episodes, log_interval, eval_interval, steps_p
     gathered so all ranks count the same episodes and stop after the same update, and rank 0
     alone evaluates and writes artifacts."""
     from ppo.agent import RolloutBuffer
+    from ppo.rollout import LockstepRollout
 
     group = getattr(agent, "_dist", None)
     rank, world = _rank_world(group)
@@ -321,19 +322,12 @@ def _train_vector(env, agent, max_episodes, log_interval, eval_interval, steps_p
     base.set_seed_schedule(exp_seed)
     obs, _ = env.reset()
     buf.states[0].copy_(obs.reshape(E, sd))
+    roll = LockstepRollout(agent, base, buf, use_graph=getattr(agent, "use_graphs", True))
     episode_rewards, training_episodes = [], []
     total_steps = episode_num = 0
     while episode_num < max_episodes:
         t_update = time.time()
-        buf.draw_noise(agent.generator)
-        for t in range(T):
-            agent.select_action(buf.states[t], out=(buf.actions[t], buf.pre_tanh[t],
-                                                    buf.log_probs[t], buf.values[t]),
-                                noise=buf.noise[t])
-            base.step_into(buf.actions[t], buf.states[t + 1].view(E, *base.obs_buf.shape[1:]),
-                           buf.rewards[t], buf.terminated[t], buf.truncated[t],
-                           buf.ep_return[t], buf.ep_length[t])
-        buf.finish_dones()
+        roll.run()
         total_steps += T * E * world
         upd = agent.update_rollout(buf, agent.value(buf.states[T]))
         # episode bookkeeping, in (step, global env) order -- identical on every rank
