@@ -36,7 +36,7 @@ def test_cli_defaults(monkeypatch):
     a = b.parse()
     assert (a.gpus, a.steps, a.warmup, a.config, a.hidden, a.epochs, a.minibatches) == \
         (1, 5, 2, 1, 256, 8, 32)
-    assert b.CONFIGS[1] == dict(envs=4096, obs=15, order="sorted", pe="none", d=0)
+    assert b.CONFIGS[1] == dict(envs=4096, obs=15, order="sorted", pe="none", d=0, rollout=128)
 
 
 def test_config_table_matches_baseline_json():

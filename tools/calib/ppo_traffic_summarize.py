@@ -1,5 +1,6 @@
 """Per-minibatch-step HBM-side traffic of the fused PPO update from tools/pmc_ppo_traffic.sh
-    python3 tools/calib/ppo_traffic_summarize.py gpurun_out/pmc_ppo  -> profiles/ppo_step_pmc.json
+    python3 tools/calib/ppo_traffic_summarize.py gpurun_out/pmc_ppo [rows]
+        -> profiles/ppo_step_pmc.json (4096 rows) or profiles/ppo_step_pmc_<rows>.json
 
 FETCH_SIZE / WRITE_SIZE count the L2's memory-side requests (Infinity-Cache hits included).
 On gfx950 FETCH_SIZE reports half the bytes of 16-B-per-lane streaming reads, which is how
@@ -9,6 +10,7 @@ are uncalibrated (0.85 MB of the step's writes)."""
 import collections, csv, glob, json, os, sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_ppo"
+rows = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
@@ -23,12 +25,14 @@ for k, cs in agg.items():
     per[k] = {"fetch_size_raw_bytes": fetch, "write_size_raw_bytes": write,
               "read_bytes": 2 * fetch, "write_bytes": write, "launches": len(cs["FETCH_SIZE"])}
 tot = sum(v["read_bytes"] + v["write_bytes"] for v in per.values())
-res = {"kernel": "PPO minibatch step (4096 rows, S=60, H=256)", "per_kernel": per,
+res = {"kernel": f"PPO minibatch step ({rows} rows, S=60, H=256)", "rows": rows, "S": 60, "H": 256,
+       "per_kernel": per,
        "hbm_side_bytes_per_step": tot,
        "method": ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
-                  "tools/probe_ppo_time.py 256 2 (tools/pmc_ppo_traffic.sh); FETCH_SIZE x2 for "
+                  "tools/probe_ppo_time.py 256 2 <rows> (tools/pmc_ppo_traffic.sh); FETCH_SIZE x2 for "
                   "16-B-per-lane reads, WRITE_SIZE as is; counts L2 memory-side requests, so "
                   "Infinity-Cache hits are included")}
 os.makedirs("profiles", exist_ok=True)
-json.dump(res, open("profiles/ppo_step_pmc.json", "w"), indent=1)
+out = "profiles/ppo_step_pmc.json" if rows == 4096 else f"profiles/ppo_step_pmc_{rows}.json"
+json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))

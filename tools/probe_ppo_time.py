@@ -1,5 +1,6 @@
 """Times the fused PPO update (graph of ppo_rows / ppo_wgrad / ppo_wsum / ppo_adam) at the bench
-minibatch (development aid): probe_ppo_time.py [H] [reps]; HWY_LIB overrides the library."""
+minibatch (development aid): probe_ppo_time.py [H] [reps] [minibatch rows]; HWY_LIB overrides
+the library."""
 import os, sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "highway-rope-ppo_amd"))
@@ -12,7 +13,8 @@ from hwy.ppo_native import FusedPPO
 from ppo.agent import PPOAgent
 
 dev = torch.device("cuda", 0)
-S, H, mb, nmb = 60, int(sys.argv[1]) if len(sys.argv) > 1 else 256, 4096, 32
+S, H, nmb = 60, int(sys.argv[1]) if len(sys.argv) > 1 else 256, 32
+mb = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 torch.manual_seed(0)
 ag = PPOAgent(S, 2, lr=3e-4, epochs=1, hidden_dim=H, device=dev, use_graphs=False, backend="hip")

@@ -12,5 +12,6 @@ timeout -k 10 ${RUN_LIMIT:-900} python -u tools/train_parity.py --seeds ${SEEDS:
   --eval-interval $(( EPISODES / 30 )) --out "$OUT" > "$OUT/train.log" 2>&1
 rc=$?
 find "$OUT" -name '*.pth' -delete
+find "$OUT" -type d -name artifacts -prune -exec rm -rf {} +  # per-episode JSON / plots: large
 grep '"final_reward"\|mean_final' "$OUT/train.log" | cut -c1-300
 exit $rc

@@ -79,7 +79,7 @@ def main():
         hp.entropy_coef = 0.005
         if args.rollout:
             hp.steps_per_update = args.num_envs * args.rollout
-        extra = {"log_interval": 50, "eval_interval": args.eval_interval}
+        extra = {"log_interval": max(50, args.episodes // 200), "eval_interval": args.eval_interval}
         if args.num_envs > 1:
             extra["num_envs"] = args.num_envs
         if args.minibatches:
