@@ -18,6 +18,7 @@
 // All GEMMs use v_mfma_f32_*_f32: exact fp32 products, fp32 accumulation.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <type_traits>
@@ -415,9 +416,22 @@ struct Work {
   int nhead, HP, sa, s2, s1, ca, c2, c1, nred;
   // fused path (ppo_rows + ppo_wgrad)
   bool fused;
-  int n1, tac, t2, t1, nh, split, grid2, nred2;
+  int rt, n1, tac, t2, t1, nh, split, grid2, nred2;  // rt: rows per ppo_rows workgroup
   int sb, hb;  // ring blocks of the row kernels (rows_blocks)
 };
+
+// minibatch rows per ppo_rows workgroup: 32 (two 16-row blocks sharing every weight register
+// block: half the weight stream per row) when the grid still covers the chip and the LDS images
+// fit (H <= 256), else 16.  HWY_ROWS_RT=16|32 forces one (development A/B).
+inline int rows_tile(int B, int H) {
+  static const int force = [] {
+    const char* e = getenv("HWY_ROWS_RT");
+    return e ? atoi(e) : 0;
+  }();
+  if (H > 256) return kRowTile;
+  if (force == 16 || force == 32) return force;
+  return B >= 8192 ? 2 * kRowTile : kRowTile;
+}
 
 // the fused row path covers the reference's shapes: float4 state rows, H a multiple of 64
 inline bool fused_ok(const hwy_ppo_dims& d) {
@@ -447,7 +461,8 @@ inline Work carve(const hwy_ppo_dims& d, void* ws, int64_t* bytes_out) {
   const Layout L = make_layout(d);
   w.nred = (int)((L.numel + kRedThreads - 1) / kRedThreads);
   w.fused = fused_ok(d);
-  w.n1 = (B + kRowTile - 1) / kRowTile;
+  w.rt = rows_tile(B, H);
+  w.n1 = (B + w.rt - 1) / w.rt;
   const int tmh = (H + kWgTM - 1) / kWgTM, tnh = (H + kWgTN - 1) / kWgTN;
   w.tac = ((2 * H + kWgTM - 1) / kWgTM) * tnh;
   w.t2 = tmh * tnh;
@@ -731,25 +746,38 @@ struct WRing {
     for (int d = 0; d < D; ++d) load_ahead<0>(d, buf[d]);
     __builtin_amdgcn_sched_barrier(0);
   }
-  // acc += act[16][16*nblk] (LDS, pitch pa) x segment SEG's weights for this wave's columns
-  template <int SEG>
-  __device__ __forceinline__ void run(const float* act, int pa, f32x4 (&acc)[TW]) {
+  // acc += act[16 RB][16*nblk] (LDS, pitch pa) x segment SEG's weights for this wave's columns;
+  // the RB 16-row blocks share every weight register block (RB = 2 halves the weight stream
+  // per row)
+  template <int SEG, int RB>
+  __device__ __forceinline__ void run(const float* act, int pa, f32x4 (&acc)[RB][TW]) {
     const int nblk = sg[SEG].nblk;
     const float* arow = act + c * pa + 4 * g;
-    f32x4 a_nxt = *reinterpret_cast<const f32x4*>(arow);
+    f32x4 a_nxt[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+      a_nxt[rb] = *reinterpret_cast<const f32x4*>(arow + 16 * rb * pa);
     for (int b0 = 0; b0 < nblk; b0 += D) {
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         const int kb = 16 * (b0 + d);
-        const f32x4 a = a_nxt;  // activations of this block, read one block ahead
-        a_nxt = *reinterpret_cast<const f32x4*>(arow + min(kb + 16, 16 * (nblk - 1)));
+        f32x4 a[RB];  // activations of this block, read one block ahead
+        const int kn = min(kb + 16, 16 * (nblk - 1));
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+          a[rb] = a_nxt[rb];
+          a_nxt[rb] = *reinterpret_cast<const f32x4*>(arow + 16 * rb * pa + kn);
+        }
         const bool kin = kb + 4 * g < sg[SEG].K;  // else the block was clamped: weights are 0
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int t = 0; t < TW; ++t)
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], kin ? buf[d][t][j] : 0.0f,
-                                                          acc[t], 0, 0, 0);
+          for (int t = 0; t < TW; ++t) {
+            const float bw = kin ? buf[d][t][j] : 0.0f;
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb)
+              acc[rb][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rb][j], bw, acc[rb][t], 0, 0, 0);
+          }
         // issue the refill here: the scheduler would otherwise sink it next to its use
         __builtin_amdgcn_sched_barrier(0);
         load_ahead<SEG>(b0 + d + D, buf[d]);
@@ -759,10 +787,12 @@ struct WRing {
   }
 };
 
-template <int TW>
-__device__ __forceinline__ void zero_acc(f32x4 (&acc)[TW]) {
+template <int RB, int TW>
+__device__ __forceinline__ void zero_acc(f32x4 (&acc)[RB][TW]) {
 #pragma unroll
-  for (int t = 0; t < TW; ++t) acc[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int t = 0; t < TW; ++t) acc[rb][t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 }
 
 template <int TW>
@@ -799,43 +829,45 @@ __device__ __forceinline__ void ring_setup(WRing<TW, D, NSEG, TL>& R, const floa
   for (int i = 0; i < NSEG; ++i) R.sg[i] = all[i];
 }
 
-// C element (t, r) of lane: row 4*(lane>>4) + r, column n_base + 16 t + (lane & 15)
-template <int QH>
-__device__ __forceinline__ void row_epi_bias_relu(const f32x4 (&acc)[QH], const float (&bias)[QH],
-                                                  float* out, int po, float* gout, int ldg,
-                                                  int nrows, int n_base) {
+// C element (rb, t, r) of lane: row 16 rb + 4*(lane>>4) + r, column n_base + 16 t + (lane & 15)
+template <int RB, int TW>
+__device__ __forceinline__ void row_epi_bias_relu(const f32x4 (&acc)[RB][TW],
+                                                  const float (&bias)[TW], float* out, int po,
+                                                  int n_base) {
   const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
 #pragma unroll
-  for (int t = 0; t < QH; ++t) {
-    const int n = n_base + 16 * t + c;
-    const float bn = bias[t];
+  for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = 4 * g + r;
-      float v = acc[t][r] + bn;
-      v = v > 0.0f ? v : 0.0f;
-      out[row * po + n] = v;
-      if (gout && row < nrows) gout[(long)row * ldg + n] = v;
+    for (int t = 0; t < TW; ++t) {
+      const int n = n_base + 16 * t + c;
+      const float bn = bias[t];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * rb + 4 * g + r;
+        float v = acc[rb][t][r] + bn;
+        v = v > 0.0f ? v : 0.0f;
+        out[row * po + n] = v;
+      }
     }
-  }
 }
 
-template <int QH>
-__device__ __forceinline__ void row_epi_mask(const f32x4 (&acc)[QH], float* mask_inout, int pm,
-                                             bool write_lds, float* gout, int ldg, int nrows,
+// the layer's output gradient through the ReLU mask of its forward activation, in place
+template <int RB, int TW>
+__device__ __forceinline__ void row_epi_mask(const f32x4 (&acc)[RB][TW], float* mask_inout, int pm,
                                              int n_base) {
   const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
 #pragma unroll
-  for (int t = 0; t < QH; ++t) {
-    const int n = n_base + 16 * t + c;
+  for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = 4 * g + r;
-      const float v = mask_inout[row * pm + n] > 0.0f ? acc[t][r] : 0.0f;
-      if (write_lds) mask_inout[row * pm + n] = v;
-      if (gout && row < nrows) gout[(long)row * ldg + n] = v;
+    for (int t = 0; t < TW; ++t) {
+      const int n = n_base + 16 * t + c;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * rb + 4 * g + r;
+        const float v = mask_inout[row * pm + n] > 0.0f ? acc[rb][t][r] : 0.0f;
+        mask_inout[row * pm + n] = v;
+      }
     }
-  }
 }
 
 // 16-B store of a row-kernel output (write-through sc1 stores measured no faster here)
@@ -843,21 +875,21 @@ __device__ __forceinline__ void st_f4(float* p, f32x4 v) { *reinterpret_cast<f32
 
 // rows 0 .. nrows-1 of an LDS image (pitch floats, ncols % 4 == 0) to HBM rows of ldg floats:
 // whole 16-B segments, consecutive lanes on consecutive segments of a row
-template <int NT>
+template <int NT, int RT>
 __device__ __forceinline__ void rows_out(const float* img, int pitch, float* g, int ldg, int ncols,
                                          int nrows) {
   const int per_row = ncols / 4;
-  for (int e = threadIdx.x; e < kRowTile * per_row; e += NT) {
+  for (int e = threadIdx.x; e < RT * per_row; e += NT) {
     const int row = e / per_row, c4 = (e - row * per_row) * 4;
     if (row < nrows)
       st_f4(g + (long)row * ldg + c4, *reinterpret_cast<const f32x4*>(&img[row * pitch + c4]));
   }
 }
 
-// Forward of the 16 rows starting at row0 (rows idx[row0 + i], or row0 + i without idx) into
+// Forward of the RT rows starting at row0 (rows idx[row0 + i], or row0 + i without idx) into
 // the LDS images X, H1, H2, AC = [a1 | c1]; optionally also to HBM (xg, h1, h2; null = no).
-// Ends with a workgroup barrier.
-template <int QH, int NW, int D, int NSEG, bool TL>
+// X may alias AC (it is dead once h1 is computed).  Ends with a workgroup barrier.
+template <int QH, int NW, int RT, int D, int NSEG, bool TL>
 __device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG, TL>& R, const float* states,
                                              const int64_t* idx, int S, int nrows, int row0,
                                              const float* P, const int64_t* off, float* X,
@@ -866,6 +898,7 @@ __device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG, TL>& R
   constexpr int H = 64 * QH;
   constexpr int TW = H_TW(QH, NW);
   constexpr int NT = 64 * NW;
+  constexpr int RB = RT / 16;
   constexpr int PH = H + 4, PA = 2 * H + 4;
   const int t = threadIdx.x;
   // this wave's bias values of the four layers, loaded ahead of their epilogues
@@ -880,8 +913,8 @@ __device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG, TL>& R
   }
   // zero-padded to whole ring groups of 16-deep blocks
   const int Sp = ((S + 15) / 16 + D - 1) / D * D * 16, px = row_pitch(Sp);
-  // states rows, zero-padded to Sp columns and 16 rows
-  for (int e = t; e < kRowTile * (Sp / 4); e += NT) {
+  // states rows, zero-padded to Sp columns and RT rows
+  for (int e = t; e < RT * (Sp / 4); e += NT) {
     const int row = e / (Sp / 4), k = 4 * (e % (Sp / 4));
     f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
     if (row < nrows && k < S) {
@@ -894,54 +927,59 @@ __device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG, TL>& R
   __syncthreads();
   PSEC(0);
   const int nb = R.n_base;  // this wave's output columns of an H-wide layer
-  f32x4 acc[TW];
+  f32x4 acc[RB][TW];
   // h1 = relu(x W1^T + b1)
   zero_acc(acc);
   R.template run<0>(X, px, acc);
-  row_epi_bias_relu<TW>(acc, bias[0], H1, PH, nullptr, H, nrows, nb);
+  row_epi_bias_relu(acc, bias[0], H1, PH, nb);
   __syncthreads();
-  if (h1g) rows_out<NT>(H1, PH, h1g + (long)row0 * H, H, H, nrows);
+  if (h1g) rows_out<NT, RT>(H1, PH, h1g + (long)row0 * H, H, H, nrows);
   PSEC(1);
   // h2 = relu(h1 W2^T + b2)
   zero_acc(acc);
   R.template run<1>(H1, PH, acc);
-  row_epi_bias_relu<TW>(acc, bias[1], H2, PH, nullptr, H, nrows, nb);
+  row_epi_bias_relu(acc, bias[1], H2, PH, nb);
   __syncthreads();
-  if (h2g) rows_out<NT>(H2, PH, h2g + (long)row0 * H, H, H, nrows);
+  if (h2g) rows_out<NT, RT>(H2, PH, h2g + (long)row0 * H, H, H, nrows);
   PSEC(2);
-  // [a1 | c1] = relu(h2 [Wa1; Wc1]^T + [ba1; bc1])
+  // [a1 | c1] = relu(h2 [Wa1; Wc1]^T + [ba1; bc1])  (X may alias AC: X is dead since layer 1)
   zero_acc(acc);
   R.template run<2>(H2, PH, acc);
-  row_epi_bias_relu<TW>(acc, bias[2], AC, PA, nullptr, 0, nrows, nb);
+  row_epi_bias_relu(acc, bias[2], AC, PA, nb);
   zero_acc(acc);
   R.template run<3>(H2, PH, acc);
-  row_epi_bias_relu<TW>(acc, bias[3], AC + H, PA, nullptr, 0, nrows, nb);
+  row_epi_bias_relu(acc, bias[3], AC + H, PA, nb);
   __syncthreads();
 }
 
-template <int QH, int NW>
+template <int QH, int NW, int RT>
 __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   constexpr int H = 64 * QH;
   constexpr int TW = H / NW / 16;        // 16-column output tiles per wave
-  constexpr int RPW = kRowTile / NW;     // loss-head rows per wave
+  constexpr int RB = RT / 16;            // 16-row blocks per workgroup
+  constexpr int RPW = RT / NW;           // loss-head rows per wave
   constexpr int NT = 64 * NW;            // threads
   constexpr int WPS = 3 * H + 16;        // per-wave head-partial stride (LDS)
   static_assert(TW * 16 * NW == H, "H must split into 16-column tiles per wave");
+  static_assert(RT % 16 == 0 && RPW >= 1, "RT: whole 16-row blocks, a loss-head row per wave");
   constexpr int PH = H + 4, PA = 2 * H + 4, PXMAX = kMaxRowS + 4;
   // the waves' head partials are combined in the [a1|c1] image (free by then), or in a separate
-  // array when NW waves' partials do not fit it
-  constexpr bool kOwnHP = NW * WPS > kRowTile * PA;
-  __shared__ __attribute__((aligned(16))) float X[kRowTile * PXMAX];
-  __shared__ __attribute__((aligned(16))) float H1[kRowTile * PH];
-  __shared__ __attribute__((aligned(16))) float H2[kRowTile * PH];
-  __shared__ __attribute__((aligned(16))) float AC[kRowTile * PA];
+  // array when NW waves' partials do not fit it; the states image lives in [a1|c1] too when its
+  // rows fit (it is dead before [a1|c1] is written)
+  constexpr bool kOwnHP = NW * WPS > RT * PA;
+  constexpr bool kOwnX = PXMAX > PA;
+  __shared__ __attribute__((aligned(16))) float XX[kOwnX ? RT * PXMAX : 4];
+  __shared__ __attribute__((aligned(16))) float H1[RT * PH];
+  __shared__ __attribute__((aligned(16))) float H2[RT * PH];
+  __shared__ __attribute__((aligned(16))) float AC[RT * PA];
   __shared__ float HPX[kOwnHP ? NW * WPS : 1];
   float* HPW = kOwnHP ? HPX : AC;
+  float* X = kOwnX ? XX : AC;
   PSEC_DECL
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int S = r.S;
-  const int row0 = blockIdx.x * kRowTile;
-  const int nrows = min(kRowTile, r.B - row0);
+  const int row0 = blockIdx.x * RT;
+  const int nrows = min(RT, r.B - row0);
   const float* P = r.params;
   constexpr int D = ring_depth<TW>();
   WRing<TW, D, 7, true> R;
@@ -971,11 +1009,11 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   }
   const float ba0 = P[r.off[P_BA2]], ba1 = P[r.off[P_BA2] + 1], bcv = P[r.off[P_BC2]];
   const float ls0 = P[r.off[P_LOGSTD]], ls1 = P[r.off[P_LOGSTD] + 1];
-  rows_forward<QH, NW>(R, r.states, r.idx, S, nrows, row0, P, r.off, X, H1, H2, AC, r.xg, r.h1,
-                       r.h2 PSEC_ARGS);
+  rows_forward<QH, NW, RT>(R, r.states, r.idx, S, nrows, row0, P, r.off, X, H1, H2, AC, r.xg,
+                           r.h1, r.h2 PSEC_ARGS);
   PSEC(3);
   const int nb = w * (H / NW);  // this wave's output columns of an H-wide layer
-  f32x4 acc[TW];
+  f32x4 acc[RB][TW];
 
   // ---- loss head (ppo/agent.py:226-245): wave w takes rows RPW*w ..; lane owns the hidden
   // columns lane + 64q; dL/d[a1|c1] overwrites [a1|c1] in LDS (and goes to HBM for ppo_wgrad);
@@ -1086,16 +1124,16 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
     }
   }
   __syncthreads();
-  rows_out<NT>(AC, PA, r.dac + (long)row0 * 2 * H, 2 * H, 2 * H, nrows);
+  rows_out<NT, RT>(AC, PA, r.dac + (long)row0 * 2 * H, 2 * H, 2 * H, nrows);
   PSEC(4);
   // dh2 = (dac [Wa1; Wc1]) * (h2 > 0)   ([Wa1; Wc1] is [2H][H]: k-major); the two halves of
   // K = 2H (Wa1 rows, Wc1 rows) are summed at the end
   zero_acc(acc);
   R.template run<4>(AC, PA, acc);
   R.template run<5>(AC + H, PA, acc);
-  row_epi_mask<TW>(acc, H2, PH, true, nullptr, H, nrows, nb);
+  row_epi_mask(acc, H2, PH, nb);
   __syncthreads();
-  if (r.dh2) rows_out<NT>(H2, PH, r.dh2 + (long)row0 * H, H, H, nrows);
+  if (r.dh2) rows_out<NT, RT>(H2, PH, r.dh2 + (long)row0 * H, H, H, nrows);
   PSEC(5);
   // the head partials of the NW waves -> one row per workgroup (fixed order); [a1|c1] is free
   {
@@ -1124,9 +1162,9 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   // dh1 = (dh2 W2) * (h1 > 0)
   zero_acc(acc);
   R.template run<6>(H2, PH, acc);
-  row_epi_mask<TW>(acc, H1, PH, true, nullptr, H, nrows, nb);  // dh1 over h1 (same thread)
+  row_epi_mask(acc, H1, PH, nb);  // dh1 over h1 (same thread)
   __syncthreads();
-  if (r.dh1) rows_out<NT>(H1, PH, r.dh1 + (long)row0 * H, H, H, nrows);
+  if (r.dh1) rows_out<NT, RT>(H1, PH, r.dh1 + (long)row0 * H, H, H, nrows);
   PSEC(6);
   PSEC_FLUSH;
 }
@@ -1166,8 +1204,8 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_act(ActArgs r) {
 #ifdef HWY_SECTION_PROFILE
   uint64_t _pt = 0, _pacc[16];
 #endif
-  rows_forward<QH, NW>(R, r.states, nullptr, r.S, nrows, row0, P, r.off, X, H1, H2, AC, nullptr,
-                       nullptr, nullptr PSEC_ARGS);
+  rows_forward<QH, NW, kRowTile>(R, r.states, nullptr, r.S, nrows, row0, P, r.off, X, H1, H2, AC,
+                                 nullptr, nullptr, nullptr PSEC_ARGS);
   float wa0[QH], wa1[QH], wc[QH];
 #pragma unroll
   for (int q = 0; q < QH; ++q) {
@@ -1901,15 +1939,24 @@ int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
     r.counters = a->counters;
     // 8 waves (2 per SIMD) when the columns split into 16-wide tiles, else 4
     const dim3 g1(w.n1), b4(256), b8(512), blk(256);
-    switch (H / 64) {
-      case 1: hipLaunchKernelGGL((ppo_rows<1, 4>), g1, b4, 0, s, r); break;
-      case 2: hipLaunchKernelGGL((ppo_rows<2, 8>), g1, b8, 0, s, r); break;
-      case 3: hipLaunchKernelGGL((ppo_rows<3, 4>), g1, b4, 0, s, r); break;
-      case 4: hipLaunchKernelGGL((ppo_rows<4, HWY_ROWS_NW>), g1, dim3(64 * HWY_ROWS_NW), 0, s, r); break;
-      case 5: hipLaunchKernelGGL((ppo_rows<5, 4>), g1, b4, 0, s, r); break;
-      case 6: hipLaunchKernelGGL((ppo_rows<6, 8>), g1, b8, 0, s, r); break;
-      case 7: hipLaunchKernelGGL((ppo_rows<7, 4>), g1, b4, 0, s, r); break;
-      default: hipLaunchKernelGGL((ppo_rows<8, 8>), g1, b8, 0, s, r); break;
+    if (w.rt == 2 * kRowTile) {
+      switch (H / 64) {
+        case 1: hipLaunchKernelGGL((ppo_rows<1, 4, 32>), g1, b4, 0, s, r); break;
+        case 2: hipLaunchKernelGGL((ppo_rows<2, 8, 32>), g1, b8, 0, s, r); break;
+        case 3: hipLaunchKernelGGL((ppo_rows<3, 4, 32>), g1, b4, 0, s, r); break;
+        default: hipLaunchKernelGGL((ppo_rows<4, 8, 32>), g1, b8, 0, s, r); break;
+      }
+    } else {
+      switch (H / 64) {
+        case 1: hipLaunchKernelGGL((ppo_rows<1, 4, 16>), g1, b4, 0, s, r); break;
+        case 2: hipLaunchKernelGGL((ppo_rows<2, 8, 16>), g1, b8, 0, s, r); break;
+        case 3: hipLaunchKernelGGL((ppo_rows<3, 4, 16>), g1, b4, 0, s, r); break;
+        case 4: hipLaunchKernelGGL((ppo_rows<4, HWY_ROWS_NW, 16>), g1, dim3(64 * HWY_ROWS_NW), 0, s, r); break;
+        case 5: hipLaunchKernelGGL((ppo_rows<5, 4, 16>), g1, b4, 0, s, r); break;
+        case 6: hipLaunchKernelGGL((ppo_rows<6, 8, 16>), g1, b8, 0, s, r); break;
+        case 7: hipLaunchKernelGGL((ppo_rows<7, 4, 16>), g1, b4, 0, s, r); break;
+        default: hipLaunchKernelGGL((ppo_rows<8, 8, 16>), g1, b8, 0, s, r); break;
+      }
     }
     rc |= hipGetLastError() == hipSuccess ? 0 : -1;
     WgArgs g = {};

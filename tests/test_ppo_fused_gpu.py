@@ -96,7 +96,11 @@ def _check_grads(ga, gb, g64, msg=""):
                                     (60, 192, 200), (30, 128, 256),  # split-K path (S % 4)
                                     # configs[4]'s learner shapes: N=30 rows of F_out 4 (none /
                                     # RoPE) or 8 (RankPE / DistPE, d 4), hidden 256 / 384 / 512
-                                    (120, 384, 4096), (240, 256, 4096), (240, 512, 4096)])
+                                    (120, 384, 4096), (240, 256, 4096), (240, 512, 4096),
+                                    # 32-row ppo_rows workgroups (rows >= 8192, H <= 256): the
+                                    # bench minibatch, S = 240, ragged last workgroups (8 / 16 rows)
+                                    (60, 256, 16384), (240, 256, 8192), (136, 192, 8200),
+                                    (60, 64, 8208)])
 def test_fused_gradient_matches_autograd(S, H, mb):
     """One fused forward/backward against autograd on the same minibatch.  The reference
     gradient is float64 autograd: at S = 240 / H = 512 and 4096 rows torch's own fp32 GEMMs

@@ -1,4 +1,5 @@
-"""Per-phase shader-clock breakdown of ppo_rows / ppo_wgrad (development aid).
+"""Per-phase shader-clock breakdown of ppo_rows / ppo_wgrad (development aid):
+probe_ppo_sections.py [H] [minibatch rows]; HWY_ROWS_RT=16|32 forces ppo_rows' row tile.
 
 Needs the profiling build: make -C highway-rope-ppo_amd/csrc prof  (-> hwy/libhwy_prof.so).
 """
@@ -13,7 +14,8 @@ from hwy.ppo_native import FusedPPO
 from ppo.agent import PPOAgent
 
 dev = torch.device("cuda", 0)
-S, H, mb, nmb = 60, int(sys.argv[1]) if len(sys.argv) > 1 else 256, 4096, 32
+S, H, nmb = 60, int(sys.argv[1]) if len(sys.argv) > 1 else 256, 32
+mb = int(sys.argv[2]) if len(sys.argv) > 2 else 4096  # minibatch rows
 torch.manual_seed(0)
 ag = PPOAgent(S, 2, lr=3e-4, epochs=1, hidden_dim=H, device=dev, use_graphs=False, backend="hip")
 n = mb * nmb
@@ -40,7 +42,9 @@ torch.cuda.synchronize()
 L.hwy_ppo_debug_sections(buf, 1)
 steps = reps * nmb
 print(f"H={H}: {ev0.elapsed_time(ev1) / steps * 1e3:.1f} us per minibatch step (graph, incl. adam)")
-n1 = (mb + 15) // 16
+rt = int(os.environ.get("HWY_ROWS_RT", "0")) or (32 if H <= 256 and mb >= 8192 else 16)
+n1 = (mb + rt - 1) // rt  # ppo_rows workgroups (rows_tile in ppo_kernels.hip)
+print(f"  ppo_rows: {rt} rows per workgroup, {n1} workgroups")
 names = {0: "rows: gather", 1: "rows: h1", 2: "rows: h2", 3: "rows: ac", 7: "rows: head sums",
          11: "rows: head rows", 4: "rows: head sync", 5: "rows: dh2", 6: "rows: dh1"}
 tot = sum(buf[i] for i in names)
