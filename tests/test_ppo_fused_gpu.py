@@ -100,7 +100,9 @@ def _check_grads(ga, gb, g64, msg=""):
                                     # 32-row ppo_rows workgroups (rows >= 8192, H <= 256): the
                                     # bench minibatch, S = 240, ragged last workgroups (8 / 16 rows)
                                     (60, 256, 16384), (240, 256, 8192), (136, 192, 8200),
-                                    (60, 64, 8208)])
+                                    (60, 64, 8208),
+                                    # several row tiles per ppo_rows workgroup (16-row tiles)
+                                    (60, 384, 8192)])
 def test_fused_gradient_matches_autograd(S, H, mb):
     """One fused forward/backward against autograd on the same minibatch.  The reference
     gradient is float64 autograd: at S = 240 / H = 512 and 4096 rows torch's own fp32 GEMMs
