@@ -71,6 +71,9 @@ constexpr int kMaxRowS = 256;  // states dim bound of the fused path (LDS)
 #ifndef HWY_ROWS_NW
 #define HWY_ROWS_NW 8  // ppo_rows waves at H = 256 (16: 4 per SIMD, one 16-column tile each)
 #endif
+#ifndef HWY_ROWS_NW32
+#define HWY_ROWS_NW32 8  // the same for the 32-row tiles
+#endif
 constexpr int kWgTM = 128, kWgTN = 64;          // ppo_wgrad output tile
 constexpr int kWgWaves = 8;                     // ppo_wgrad waves (2 per SIMD)
 constexpr int kWgPart = kWgTM * kWgTN + kWgTM;  // floats per partial tile (+ bias sums)
@@ -1944,7 +1947,7 @@ int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
         case 1: hipLaunchKernelGGL((ppo_rows<1, 4, 32>), g1, b4, 0, s, r); break;
         case 2: hipLaunchKernelGGL((ppo_rows<2, 8, 32>), g1, b8, 0, s, r); break;
         case 3: hipLaunchKernelGGL((ppo_rows<3, 4, 32>), g1, b4, 0, s, r); break;
-        default: hipLaunchKernelGGL((ppo_rows<4, 8, 32>), g1, b8, 0, s, r); break;
+        default: hipLaunchKernelGGL((ppo_rows<4, HWY_ROWS_NW32, 32>), g1, dim3(64 * HWY_ROWS_NW32), 0, s, r); break;
       }
     } else {
       switch (H / 64) {
