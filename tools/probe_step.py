@@ -2,6 +2,10 @@
 import sys, os, time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "highway-rope-ppo_amd"))
 import torch
+import hwy.native as native
+
+if os.environ.get("HWY_LIB"):  # a variant library (development A/B)
+    native.LIB_PATH = os.environ["HWY_LIB"]
 from config.base_config import HIGHWAY_CONFIG
 from hwy.vec_env import HighwayVecEnv
 
