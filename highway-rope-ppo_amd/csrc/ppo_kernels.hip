@@ -688,7 +688,14 @@ struct RowArgs {
   int32_t* counters;
 };
 
-__device__ __forceinline__ int row_pitch(int n) { return n + 4; }  // n/4 + 1 odd: conflict-free
+// Row pitch (floats) of the row kernels' LDS images for n columns (n % 16 == 0): n + 8, i.e. a
+// quad pitch = 2 mod 4.  The MFMA operand reads (ds_read_b128, lane (g, c) reads quad
+// c * pitch/4 + g + kb/4) are serviced in the lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}
+// (+32): with a quad pitch = 1 mod 16 (n + 4) two lanes of every group land on the same four
+// banks (SQ_LDS_BANK_CONFLICT: 3.3 M cycles per 16,384-row launch); with 2 mod 4 none do.  The
+// epilogues' ds_write_b32 then meet 2-way, which costs a store nothing.
+constexpr int lds_pitch(int n) { return n + 8; }
+__device__ __forceinline__ int row_pitch(int n) { return lds_pitch(n); }
 
 // The weights of every layer a ppo_rows / ppo_act wave touches, as one stream of 16-deep k
 // blocks (segments = layers, in execution order).  D blocks stay in flight in registers and the
@@ -929,7 +936,7 @@ __device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG, TL>& R
   constexpr int TW = H_TW(QH, NW);
   constexpr int NT = 64 * NW;
   constexpr int RB = RT / 16;
-  constexpr int PH = H + 4, PA = 2 * H + 4;
+  constexpr int PH = lds_pitch(H), PA = lds_pitch(2 * H);
   const int t = threadIdx.x;
   // this wave's bias values of the four layers, loaded ahead of their epilogues
   float bias[4][TW];
@@ -1000,7 +1007,7 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   constexpr int NT = 64 * NW;            // threads
   static_assert(TW * 16 * NW == H, "H must split into 16-column tiles per wave");
   static_assert(RT % 16 == 0 && RPW >= 1 && RPW <= 16, "RT: whole 16-row blocks, <= 16 head rows per wave");
-  constexpr int PH = H + 4, PA = 2 * H + 4, PXMAX = kMaxRowS + 4;
+  constexpr int PH = lds_pitch(H), PA = lds_pitch(2 * H), PXMAX = lds_pitch(kMaxRowS);
   // the states image lives in [a1|c1] when its rows fit (it is dead before dac is written there)
   constexpr bool kOwnX = PXMAX > PA;
   __shared__ __attribute__((aligned(16))) float XX[kOwnX ? RT * PXMAX : 4];
@@ -1400,7 +1407,7 @@ template <int QH, int NW, bool TL>
 __global__ void __launch_bounds__(64 * NW, 1) ppo_act(ActArgs r) {
   constexpr int H = 64 * QH;
   constexpr int RPW = kRowTile / NW;
-  constexpr int PH = H + 4, PA = 2 * H + 4, PXMAX = kMaxRowS + 4;
+  constexpr int PH = lds_pitch(H), PA = lds_pitch(2 * H), PXMAX = lds_pitch(kMaxRowS);
   __shared__ __attribute__((aligned(16))) float X[kRowTile * PXMAX];
   __shared__ __attribute__((aligned(16))) float H1[kRowTile * PH];
   __shared__ __attribute__((aligned(16))) float H2[kRowTile * PH];
