@@ -4,9 +4,10 @@
 //
 // Fused path (S % 4 == 0, S <= 256, H a multiple of 64 up to 512): four launches, captured per
 // epoch in one HIP graph:
-//   ppo_rows   16 minibatch rows per workgroup: forward (h1, h2, [a1|c1]), the loss head
-//              (ratio, clipped surrogate, MSE, entropy, their gradients, head-parameter
-//              partials), backward data gradients (dh2, dh1); weights streamed from a tile image
+//   ppo_rows   16 or 32 minibatch rows per workgroup (rows_tile): forward (h1, h2, [a1|c1]),
+//              the loss head (ratio, clipped surrogate, MSE, entropy, their gradients,
+//              head-parameter partials), backward data gradients (dh2, dh1); weights streamed
+//              from a tile image
 //   ppo_wgrad  dW = (output gradient)^T (input) as 128x64 tiles over 8 row slices (one per XCD)
 //              plus bias column sums, the head-parameter sums and the metrics row
 //   ppo_wsum   the 8 slice partials summed in slice order, sum-of-squares partials
