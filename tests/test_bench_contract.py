@@ -35,7 +35,7 @@ def test_cli_defaults(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py"])
     a = b.parse()
     assert (a.gpus, a.steps, a.warmup, a.config, a.hidden, a.epochs, a.minibatches) == \
-        (1, 5, 2, 1, 256, 8, 32)
+        (1, 20, 5, 1, 256, 8, 32)
     assert b.CONFIGS[1] == dict(envs=4096, obs=15, order="sorted", pe="none", d=0, rollout=128)
 
 
