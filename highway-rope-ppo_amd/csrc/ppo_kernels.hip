@@ -22,6 +22,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <cmath>
 #include <type_traits>
 
 #include "hwy_ppo.h"
@@ -421,8 +422,19 @@ struct Work {
   // fused path (ppo_rows + ppo_wgrad)
   bool fused;
   int rt, n1, tac, t2, t1, nh, split, grid2, nred2;  // rt: rows per ppo_rows workgroup
+  int bal, wm, tpe, nslot;                            // ppo_wgrad's balanced partition
   int sb, hb;  // ring blocks of the row kernels (rows_blocks)
 };
+
+// ppo_wgrad's balanced partition (see ppo_wgrad); HWY_WG_BAL=0 keeps one workgroup per
+// (tile, slice) (development A/B)
+inline bool wg_balance_on() {
+  static const bool on = [] {
+    const char* e = getenv("HWY_WG_BAL");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
 
 // minibatch rows per ppo_rows workgroup: 32 (two 16-row blocks sharing every weight register
 // block: half the weight stream per row) when the grid still covers the chip and the LDS images
@@ -477,12 +489,23 @@ inline Work carve(const hwy_ppo_dims& d, void* ws, int64_t* bytes_out) {
   // each, at most 8 (one per XCD)
   w.split = std::max(1, std::min({8, 256 / ntile, (B + 63) / 64}));
   w.grid2 = ntile * w.split + w.nh;
+  // balanced partition (ppo_wgrad): 32 workgroups per slice when 16-30 tiles leave CUs idle
+  // and the slices are long enough to split; an extra pays ~1.5 chunks of pipeline fill per tile
+  w.bal = 0, w.wm = 0, w.tpe = 0, w.nslot = 1;
+  {
+    const int nck = ((B + 7) / 8 + 63) / 64;  // chunks of the longest slice
+    if (wg_balance_on() && w.split == 8 && ntile >= 16 && ntile <= 30 && nck >= 16) {
+      const int E = 32 - ntile, tpe = (ntile + E - 1) / E;
+      const int m = (int)std::ceil(tpe * (nck + 1.5) / (1.0 + tpe));
+      if (m < nck) w.bal = 1, w.wm = m, w.tpe = tpe, w.nslot = 2, w.grid2 = 8 * 32;
+    }
+  }
   w.nred2 = w.nh + ntile * (kWgTM * kWgTN / 1024);
   const int64_t head_rows = w.fused ? std::max<int64_t>(w.nhead, w.n1) : w.nhead;
   const int64_t norm_n = w.fused ? std::max(w.nred, w.nred2) : w.nred;
   // the fused path needs no split-K slabs of full weight size, only the per-split tiles
   const int64_t sa = w.fused ? 0 : w.sa, s2 = w.fused ? 0 : w.s2, s1 = w.fused ? 0 : w.s1;
-  const int64_t wg_slab_n = w.fused ? (int64_t)ntile * w.split * kWgPart : 0;
+  const int64_t wg_slab_n = w.fused ? (int64_t)ntile * w.split * w.nslot * kWgPart : 0;
   const int64_t xg_n = w.fused ? (int64_t)B * S : 0;
   rows_blocks(S, H, &w.sb, &w.hb);
   const int64_t tile_n = w.fused ? tile_geom(S, H, w.sb, w.hb).total : 0;
@@ -1515,8 +1538,9 @@ struct WgArgs {
   int nhp, HP;
   float* norm_part;     // [nh] head-sum partials, then [ntile] tile partials
   int tac, t2, t1, nh;  // 128x64 tiles per region, head-sum workgroups
-  int split;            // minibatch-row slices per tile (workgroups per tile)
-  float* slab;          // [tiles][split][128*64 + 128] partial tiles + bias partials
+  int split;            // minibatch-row slices per tile (one per XCD at the bench shapes)
+  int bal, wm, tpe, nslot;  // balanced partition (ppo_wgrad): main chunks, tail tiles per extra
+  float* slab;          // [tiles][split][nslot][128*64 + 128] partial tiles + bias partials
   float entropy_coef, value_coef, ent_const;
   const float* params;
   float* metrics;
@@ -1606,23 +1630,18 @@ __device__ void wgrad_head(const WgArgs& a, int hid, float* lds, float* red) {
 }
 
 #define WG_ST(p, v) (*(p) = (v))  // (nontemporal partial stores measured slower in ppo_wsum)
-__global__ void __launch_bounds__(512) ppo_wgrad(WgArgs a) {
-  PSEC_DECL
-  __shared__ __attribute__((aligned(16))) float wg_lds[2 * (kWgTM + kWgTN) * 64];
-  __shared__ float red[kWgWaves];
+
+// Rows [kb0, kb1) of output tile tile_id into the partial tile `part` (+ the bias column sums
+// when the tile owns a bias column); an empty range writes a zero partial.
+__device__ __forceinline__ void wgrad_tile(const WgArgs& a, int tile_id, int kb0, int kb1,
+                                           float* part, float* wg_lds PSEC_PARAMS) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, l32 = lane & 31;
   const int H = a.H;
-  const int ntile = a.tac + a.t2 + a.t1;
-  int id = blockIdx.x;
-  if (id >= ntile * a.split) {  // ---- head parameters + metrics
-    wgrad_head(a, id - ntile * a.split, wg_lds, red);
-    PSEC(10);
-    PSEC_FLUSH;
+  if (kb1 <= kb0) {
+    for (int i = t; i < kWgPart; i += 64 * kWgWaves) part[i] = 0.0f;
     return;
   }
-  const int z = id % a.split;
-  const int tile_id = id / a.split;
-  id = tile_id;
+  int id = tile_id;
   const float *A, *Bm;
   int lda, ldb, M, N, ntj;
   if (id < a.tac) {  // dWac = dac^T h2
@@ -1637,9 +1656,7 @@ __global__ void __launch_bounds__(512) ppo_wgrad(WgArgs a) {
   ntj = (N + kWgTN - 1) / kWgTN;
   const int ti = id / ntj, tj = id % ntj;
   const int i0 = ti * kWgTM, j0 = tj * kWgTN;
-  const int rows = (a.B + a.split - 1) / a.split;
-  const int kb0 = z * rows, kb1 = min(a.B, kb0 + rows);
-  const int nchunk = (kb1 - kb0 + 63) / 64;  // >= 1 (split <= B / 64)
+  const int nchunk = (kb1 - kb0 + 63) / 64;  // >= 1
 
   // staging (64-row chunks): A = 64 rows x 128 features, thread: features 4ca .. 4ca+3 of rows
   // 8w + 4ra .. +3; B = 64 rows x 64 features, waves 0-3, thread: features 4cb.. of rows
@@ -1783,7 +1800,6 @@ __global__ void __launch_bounds__(512) ppo_wgrad(WgArgs a) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) bpart[(2 * w + ra) * kWgTM + 4 * ca + i] = bsum[i];
   __syncthreads();
-  float* part = a.slab + ((long)tile_id * a.split + z) * kWgPart;
   if (kh == 0) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -1799,6 +1815,60 @@ __global__ void __launch_bounds__(512) ppo_wgrad(WgArgs a) {
     WG_ST(&part[kWgTM * kWgTN + f], v);
   }
   PSEC(9);
+}
+
+// Workgroups.  Default: tile * split + z -> tile `tile`, row slice z (rows [z ceil(B / split),
+// ...)), then the head-sum workgroups.  Slice z goes to workgroups with id % 8 = z, i.e. to one
+// XCD (the dispatcher deals workgroups to the 8 XCDs round-robin), so each XCD reads one slice
+// of the activations and serves all its tiles from its own L2.
+// Balanced (a.bal; 26 tiles x 8 slices would leave 48 of 256 CUs idle): 32 workgroups per
+// slice.  Workgroup j < ntile takes tile j over the slice's first wm chunks, in lockstep with
+// the other tiles (the XCD's L2 holds the chunks they share); the 32 - ntile "extras" take the
+// remaining chunks of tpe tiles each (those chunks stay L2-resident while an extra walks its
+// tiles), into a second partial slot; the last extra of each slice also runs the head sums.
+__global__ void __launch_bounds__(512) ppo_wgrad(WgArgs a) {
+  PSEC_DECL
+  __shared__ __attribute__((aligned(16))) float wg_lds[2 * (kWgTM + kWgTN) * 64];
+  __shared__ float red[kWgWaves];
+  const int ntile = a.tac + a.t2 + a.t1;
+  const int id = blockIdx.x;
+  const int rows = (a.B + a.split - 1) / a.split;
+  if (!a.bal) {
+    if (id >= ntile * a.split) {  // ---- head parameters + metrics
+      wgrad_head(a, id - ntile * a.split, wg_lds, red);
+      PSEC(10);
+      PSEC_FLUSH;
+      return;
+    }
+    const int z = id % a.split, tile = id / a.split;
+    const int kb0 = z * rows, kb1 = min(a.B, kb0 + rows);
+    wgrad_tile(a, tile, kb0, kb1, a.slab + ((long)tile * a.split + z) * kWgPart,
+               wg_lds PSEC_ARGS);
+    PSEC_FLUSH;
+    return;
+  }
+  const int z = id % a.split, j = id / a.split;
+  const int kz = min(a.B, z * rows), kz1 = min(a.B, kz + rows), km = min(kz1, kz + 64 * a.wm);
+  auto slot = [&](int tile, int sl) {
+    return a.slab + (((long)tile * a.split + z) * a.nslot + sl) * kWgPart;
+  };
+  if (j < ntile) {
+    wgrad_tile(a, j, kz, km, slot(j, 0), wg_lds PSEC_ARGS);
+  } else {
+    const int e = j - ntile, nextra = 32 - ntile;
+    const int t0 = min(ntile, e * a.tpe), t1 = min(ntile, t0 + a.tpe);
+    for (int tile = t0; tile < t1; ++tile) {
+      if (tile > t0) __syncthreads();  // the last segment's accumulator exchange used the LDS
+      wgrad_tile(a, tile, km, kz1, slot(tile, 1), wg_lds PSEC_ARGS);
+    }
+    if (e == nextra - 1) {
+      for (int hid = z; hid < a.nh; hid += a.split) {
+        __syncthreads();
+        wgrad_head(a, hid, wg_lds, red);
+      }
+      PSEC(10);
+    }
+  }
   PSEC_FLUSH;
 }
 
@@ -1825,23 +1895,25 @@ __global__ void __launch_bounds__(256) ppo_wsum(WgArgs a) {
     if (region == 1) return a.off[P_W2] + (long)i * H;
     return a.off[P_W1] + (long)i * a.S;
   };
-  const float* sl = a.slab + (long)tile_id * a.split * kWgPart;
+  const float* sl = a.slab + (long)tile_id * a.split * a.nslot * kWgPart;
   const int e = part * 1024 + 4 * t, ri = e / kWgTN, cj = e % kWgTN;
-  constexpr int kMaxSplit = 8;
-  f32x4 pv[kMaxSplit];
+  constexpr int kMaxParts = 16;  // 8 slices x 2 slots
+  const int np = a.split * a.nslot;
+  f32x4 pv[kMaxParts];
 #pragma unroll
-  for (int zz = 0; zz < kMaxSplit; ++zz)
-    if (zz < a.split) pv[zz] = *reinterpret_cast<const f32x4*>(sl + (long)zz * kWgPart + e);
+  for (int q = 0; q < kMaxParts; ++q)
+    if (q < np) pv[q] = *reinterpret_cast<const f32x4*>(sl + (long)q * kWgPart + e);
   // the bias partials of output row i0 + t load in the same round trip as the tile's
   const bool bias_t = part == 0 && tj == 0 && t < kWgTM && i0 + t < M;
-  float bp[kMaxSplit];
+  float bp[kMaxParts];
 #pragma unroll
-  for (int zz = 0; zz < kMaxSplit; ++zz)
-    bp[zz] = (bias_t && zz < a.split) ? sl[(long)zz * kWgPart + kWgTM * kWgTN + t] : 0.0f;
+  for (int q = 0; q < kMaxParts; ++q)
+    bp[q] = (bias_t && q < np) ? sl[(long)q * kWgPart + kWgTM * kWgTN + t] : 0.0f;
+  // summed in (slice, slot) order
   f32x4 v = pv[0];
 #pragma unroll
-  for (int zz = 1; zz < kMaxSplit; ++zz)
-    if (zz < a.split) v += pv[zz];
+  for (int q = 1; q < kMaxParts; ++q)
+    if (q < np) v += pv[q];
   float sq = 0.0f;
   if (i0 + ri < M) {
     float* dst = a.grads + grad_row(i0 + ri) + j0 + cj;
@@ -1855,8 +1927,8 @@ __global__ void __launch_bounds__(256) ppo_wsum(WgArgs a) {
   if (bias_t) {  // bias of output row i0 + t
     float b = 0.0f;
 #pragma unroll
-    for (int zz = 0; zz < kMaxSplit; ++zz)
-      if (zz < a.split) b += bp[zz];
+    for (int q = 0; q < kMaxParts; ++q)
+      if (q < np) b += bp[q];
     const int i = i0 + t;
     long bo;
     if (region == 0) bo = i < H ? a.off[P_BA1] + i : a.off[P_BC1] + (i - H);
@@ -2190,6 +2262,7 @@ int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
     g.head_part = w.head_part, g.nhp = w.n1, g.HP = w.HP, g.norm_part = w.norm_part;
     g.tac = w.tac, g.t2 = w.t2, g.t1 = w.t1, g.nh = w.nh;
     g.split = w.split, g.slab = w.wg_slab;
+    g.bal = w.bal, g.wm = w.wm, g.tpe = w.tpe, g.nslot = w.nslot;
     g.entropy_coef = a->entropy_coef, g.value_coef = a->value_coef;
     g.ent_const = 0.5f + 0.91893853320467274178f;
     g.params = P, g.metrics = a->metrics, g.counters = a->counters;
