@@ -1038,17 +1038,11 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   __shared__ __attribute__((aligned(16))) float H1[RT * PH];
   __shared__ __attribute__((aligned(16))) float H2[RT * PH];
   __shared__ __attribute__((aligned(16))) float AC[RT * PA];
-  // 32-row tiles: the loss head works from the layer-3 accumulators (per-wave partial dot
-  // products of every row, the per-row output scalars, the per-wave metric / bias / log_std
-  // sums); 16-row tiles: from the [a1|c1] image, one wave per row, with the waves' head
-  // partials combined in the image after dh2 (the two measured fastest at their tile size)
-  constexpr bool kRegHead = RT == 32;
-  constexpr int WPS = 3 * H + 16;  // per-wave head-partial stride (LDS, 16-row tiles)
-  static_assert(kRegHead || NW * WPS <= RT * PA, "the head partials fit the [a1|c1] image");
-  __shared__ __attribute__((aligned(16))) f32x4 HDOT[kRegHead ? NW : 1][kRegHead ? RT : 1];
-  __shared__ __attribute__((aligned(16))) f32x4 HROW[kRegHead ? RT : 1];
-  __shared__ float HTAIL[kRegHead ? NW : 1][12];
-  float* HPW = AC;
+  // the loss head works from the layer-3 accumulators: per-wave partial dot products of every
+  // row, the per-row output scalars, the per-wave metric / bias / log_std sums
+  __shared__ __attribute__((aligned(16))) f32x4 HDOT[NW][RT];
+  __shared__ __attribute__((aligned(16))) f32x4 HROW[RT];
+  __shared__ float HTAIL[NW][12];
   float* X = kOwnX ? XX : AC;
   PSEC_DECL
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -1062,347 +1056,171 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   R.prime();
   const int nb = w * (H / NW);  // this wave's output columns of an H-wide layer
   f32x4 acc[RB][TW];
-  if constexpr (kRegHead) {
-    // the loss head's inputs and weights, loaded now so that their latency hides behind the
-    // forward: lane l < RPW of wave w holds row RPW*w + l; the head weights of this wave's
-    // output columns nb + 16t + (lane & 15)
-    const int hl = min(RPW * w + min(lane, RPW - 1), nrows - 1);
-    float hz0, hz1, hold, hadv, hret;
-    {
-      const long src = (long)r.idx[row0 + hl];
-      hz0 = r.pre_tanh[src * 2];
-      hz1 = r.pre_tanh[src * 2 + 1];
-      hold = r.old_logp[src];
-      hadv = r.adv[src];
-      hret = r.ret[src];
-    }
-    float wa0[TW], wa1[TW], wc[TW];
-  #pragma unroll
-    for (int u = 0; u < TW; ++u) {
-      const int col = w * (H / NW) + 16 * u + (lane & 15);
-      wa0[u] = P[r.off[P_WA2] + col];
-      wa1[u] = P[r.off[P_WA2] + H + col];
-      wc[u] = P[r.off[P_WC2] + col];
-    }
-    const float ba0 = P[r.off[P_BA2]], ba1 = P[r.off[P_BA2] + 1], bcv = P[r.off[P_BC2]];
-    const float ls0 = P[r.off[P_LOGSTD]], ls1 = P[r.off[P_LOGSTD] + 1];
-    f32x4 av[RB][TW], cv[RB][TW];  // a1, c1 of this wave's columns (C layout)
-    rows_forward<QH, NW, RT, true>(R, r.states, r.idx, S, nrows, row0, P, r.off, X, H1, H2, AC,
-                                   r.xg, r.h1, r.h2, av, cv PSEC_ARGS);
-    PSEC(3);
-    const int g4 = lane >> 4, c16 = lane & 15;
+  // the loss head's inputs and weights, loaded now so that their latency hides behind the
+  // forward: lane l < RPW of wave w holds row RPW*w + l; the head weights of this wave's
+  // output columns nb + 16t + (lane & 15)
+  const int hl = min(RPW * w + min(lane, RPW - 1), nrows - 1);
+  float hz0, hz1, hold, hadv, hret;
+  {
+    const long src = (long)r.idx[row0 + hl];
+    hz0 = r.pre_tanh[src * 2];
+    hz1 = r.pre_tanh[src * 2 + 1];
+    hold = r.old_logp[src];
+    hadv = r.adv[src];
+    hret = r.ret[src];
+  }
+  float wa0[TW], wa1[TW], wc[TW];
+#pragma unroll
+  for (int u = 0; u < TW; ++u) {
+    const int col = w * (H / NW) + 16 * u + (lane & 15);
+    wa0[u] = P[r.off[P_WA2] + col];
+    wa1[u] = P[r.off[P_WA2] + H + col];
+    wc[u] = P[r.off[P_WC2] + col];
+  }
+  const float ba0 = P[r.off[P_BA2]], ba1 = P[r.off[P_BA2] + 1], bcv = P[r.off[P_BC2]];
+  const float ls0 = P[r.off[P_LOGSTD]], ls1 = P[r.off[P_LOGSTD] + 1];
+  f32x4 av[RB][TW], cv[RB][TW];  // a1, c1 of this wave's columns (C layout)
+  rows_forward<QH, NW, RT, true>(R, r.states, r.idx, S, nrows, row0, P, r.off, X, H1, H2, AC,
+                                 r.xg, r.h1, r.h2, av, cv PSEC_ARGS);
+  PSEC(3);
+  const int g4 = lane >> 4, c16 = lane & 15;
 
-    // ---- loss head (ppo/agent.py:226-245).  (1) each wave's partial dot products a1 . wa2 and
-    // c1 . wc2 of every row over its columns, from the layer-3 accumulators (16-lane DPP sums);
-    // (2) the per-row scalar part, RPW rows per wave (lane = row), the partials summed in wave
-    // order; (3) dL/d[a1|c1] of this wave's columns into the [a1|c1] image for dh2 and ppo_wgrad,
-    // and the head-parameter gradients of its columns summed over the rows
-  #pragma unroll
-    for (int rb = 0; rb < RB; ++rb)
-  #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float p0 = 0.0f, p1 = 0.0f, pv = 0.0f;
-  #pragma unroll
-        for (int u = 0; u < TW; ++u) {
-          p0 += av[rb][u][q] * wa0[u];
-          p1 += av[rb][u][q] * wa1[u];
-          pv += cv[rb][u][q] * wc[u];
-        }
-        p0 = row16_sum(p0), p1 = row16_sum(p1), pv = row16_sum(pv);
-        if (c16 == 0) HDOT[w][16 * rb + 4 * g4 + q] = f32x4{p0, p1, pv, 0.0f};
-      }
-    __syncthreads();
-    PSEC(7);
-    {
-      // torch Normal: scale = exp(log_std); var = scale**2; log_scale = log(scale)
-      const float sc0 = expf(ls0), sc1 = expf(ls1);
-      const float var0 = sc0 * sc0, var1 = sc1 * sc1;
-      const float lsc0 = logf(sc0), lsc1 = logf(sc1);
-      const float LOG_SQRT_2PI = 0.91893853320467274178f;
-      const float invB = 1.0f / (float)r.B;
-      const float lo = 1.0f - r.eps_clip, hi = 1.0f + r.eps_clip;
-      const int hr = RPW * w + min(lane, RPW - 1);  // this lane's row (lanes >= RPW: a copy)
-      f32x4 dsum = HDOT[0][hr];
-  #pragma unroll
-      for (int ww = 1; ww < NW; ++ww) dsum += HDOT[ww][hr];
-      const float mu0 = dsum[0] + ba0, mu1 = dsum[1] + ba1, val = dsum[2] + bcv;
-      const float d0 = hz0 - mu0, d1 = hz1 - mu1;
-      const float t0 = tanhf(hz0), t1 = tanhf(hz1);
-      const float lp0 = -(d0 * d0) / (2.0f * var0) - lsc0 - LOG_SQRT_2PI;
-      const float lp1 = -(d1 * d1) / (2.0f * var1) - lsc1 - LOG_SQRT_2PI;
-      const float logp = (lp0 - log1pf(-(t0 * t0) + 1e-6f)) + (lp1 - log1pf(-(t1 * t1) + 1e-6f));
-      const float log_ratio = logp - hold;
-      const float ratio = expf(log_ratio);
-      const float cr = fminf(fmaxf(ratio, lo), hi);
-      const float s1 = ratio * hadv, s2 = cr * hadv;
-      const float inr = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
-      // torch.min / clamp backward: ties split the gradient evenly
-      const float wsel = s1 < s2 ? 1.0f : (s1 > s2 ? inr : 0.5f * (1.0f + inr));
-      const float dlogp = -invB * hadv * wsel * ratio;  // d(actor_loss)/d(logp)
-      // rows past nrows (and lanes past RPW) contribute nothing
-      const bool live = lane < RPW && hr < nrows;
-      const float dmu0 = live ? dlogp * d0 / var0 : 0.0f;
-      const float dmu1 = live ? dlogp * d1 / var1 : 0.0f;
-      const float dv = live ? r.value_coef * 2.0f * (val - hret) * invB : 0.0f;
-      if (lane < RPW) HROW[hr] = f32x4{dmu0, dmu1, dv, 0.0f};
-      // this wave's rows' bias / log_std gradient terms and metrics, summed over its lanes in
-      // lane order (the quad / half-row / row DPP tree over RPW <= 16 lanes)
-      float tl[9] = {dmu0, dmu1, dv,
-                     live ? dlogp * ((d0 * d0) / var0 - 1.0f) : 0.0f,
-                     live ? dlogp * ((d1 * d1) / var1 - 1.0f) : 0.0f,
-                     live ? -fminf(s1, s2) : 0.0f,
-                     live ? (val - hret) * (val - hret) : 0.0f,
-                     live ? (fabsf(ratio - 1.0f) > r.eps_clip ? 1.0f : 0.0f) : 0.0f,
-                     live ? (ratio - 1.0f) - log_ratio : 0.0f};
-  #pragma unroll
-      for (int k = 0; k < 9; ++k) {
-        const float v = row16_sum(lane < 16 ? tl[k] : 0.0f);
-        if (lane == 0) HTAIL[w][k] = v;
-      }
-      if (blockIdx.x == 0 && t == 0) {
-        r.counters[0] += 1;  // Adam step t for this minibatch
-        r.counters[1] += 1;  // metrics row (this step writes row counters[1]-1)
-      }
-    }
-    __syncthreads();
-    PSEC(11);
-    {
-      // dac of this wave's columns (the reference's expression per element), and the head
-      // weight gradients sum_rows dmu * a1 / dv * c1 of its columns: per lane over its rows, then
-      // over the four 16-lane groups
-      float ga0[TW], ga1[TW], gc[TW];
-  #pragma unroll
-      for (int u = 0; u < TW; ++u) ga0[u] = ga1[u] = gc[u] = 0.0f;
-  #pragma unroll
-      for (int rb = 0; rb < RB; ++rb)
-  #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int row = 16 * rb + 4 * g4 + q;
-          const f32x4 sc = HROW[row];
-          const float dmu0 = sc[0], dmu1 = sc[1], dv = sc[2];
-          float* arow = AC + row * PA;
-  #pragma unroll
-          for (int u = 0; u < TW; ++u) {
-            const int col = nb + 16 * u + c16;
-            const float a = av[rb][u][q], cc = cv[rb][u][q];
-            arow[col] = a > 0.0f ? (dmu0 * wa0[u] + dmu1 * wa1[u]) : 0.0f;
-            arow[H + col] = cc > 0.0f ? dv * wc[u] : 0.0f;
-            ga0[u] += dmu0 * a;
-            ga1[u] += dmu1 * a;
-            gc[u] += dv * cc;
-          }
-        }
-      float* out = r.head_part + (long)blockIdx.x * r.HP;
-  #pragma unroll
+  // ---- loss head (ppo/agent.py:226-245).  (1) each wave's partial dot products a1 . wa2 and
+  // c1 . wc2 of every row over its columns, from the layer-3 accumulators (16-lane DPP sums);
+  // (2) the per-row scalar part, RPW rows per wave (lane = row), the partials summed in wave
+  // order; (3) dL/d[a1|c1] of this wave's columns into the [a1|c1] image for dh2 and ppo_wgrad,
+  // and the head-parameter gradients of its columns summed over the rows
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float p0 = 0.0f, p1 = 0.0f, pv = 0.0f;
+#pragma unroll
       for (int u = 0; u < TW; ++u) {
-        // lanes c, c+16, c+32, c+48 hold the same column: (g0 + g1) + (g2 + g3)
-        ga0[u] += __shfl_xor(ga0[u], 16);
-        ga1[u] += __shfl_xor(ga1[u], 16);
-        gc[u] += __shfl_xor(gc[u], 16);
-        ga0[u] += __shfl_xor(ga0[u], 32);
-        ga1[u] += __shfl_xor(ga1[u], 32);
-        gc[u] += __shfl_xor(gc[u], 32);
-        if (g4 == 0) {
-          const int col = nb + 16 * u + c16;
-          out[col] = ga0[u];
-          out[H + col] = ga1[u];
-          out[2 * H + col] = gc[u];
-        }
+        p0 += av[rb][u][q] * wa0[u];
+        p1 += av[rb][u][q] * wa1[u];
+        pv += cv[rb][u][q] * wc[u];
       }
-      if (w == 0 && lane < 9) {  // the waves' tail sums in wave order
-        float v = HTAIL[0][lane];
-  #pragma unroll
-        for (int ww = 1; ww < NW; ++ww) v += HTAIL[ww][lane];
-        out[3 * H + lane] = v;
-      }
+      p0 = row16_sum(p0), p1 = row16_sum(p1), pv = row16_sum(pv);
+      if (c16 == 0) HDOT[w][16 * rb + 4 * g4 + q] = f32x4{p0, p1, pv, 0.0f};
     }
-    __syncthreads();
-    rows_out<NT, RT>(AC, PA, r.dac + (long)row0 * 2 * H, 2 * H, 2 * H, nrows);
-    PSEC(4);
-    // dh2 = (dac [Wa1; Wc1]) * (h2 > 0)   ([Wa1; Wc1] is [2H][H]: k-major); the two halves of
-    // K = 2H (Wa1 rows, Wc1 rows) are summed at the end
-    zero_acc(acc);
-    R.template run<4>(AC, PA, acc);
-    R.template run<5>(AC + H, PA, acc);
-    row_epi_mask(acc, H2, PH, nb);
-    __syncthreads();
-    if (r.dh2) rows_out<NT, RT>(H2, PH, r.dh2 + (long)row0 * H, H, H, nrows);
-    PSEC(5);
-  } else {
-    // the loss head's inputs and weights, loaded now so that their latency hides behind the
-    // forward (wave w takes rows RPW*w ..; the row values are wave-uniform)
-    float hz0[RPW], hz1[RPW], hold[RPW], hadv[RPW], hret[RPW];
-    const int wu = __builtin_amdgcn_readfirstlane(w);
-  #pragma unroll
-    for (int rr = 0; rr < RPW; ++rr) {
-      const int lr = min(RPW * wu + rr, nrows - 1);
-      const long src = (long)r.idx[row0 + lr];
-      hz0[rr] = r.pre_tanh[src * 2];
-      hz1[rr] = r.pre_tanh[src * 2 + 1];
-      hold[rr] = r.old_logp[src];
-      hadv[rr] = r.adv[src];
-      hret[rr] = r.ret[src];
+  __syncthreads();
+  PSEC(7);
+  {
+    // torch Normal: scale = exp(log_std); var = scale**2; log_scale = log(scale)
+    const float sc0 = expf(ls0), sc1 = expf(ls1);
+    const float var0 = sc0 * sc0, var1 = sc1 * sc1;
+    const float lsc0 = logf(sc0), lsc1 = logf(sc1);
+    const float LOG_SQRT_2PI = 0.91893853320467274178f;
+    const float invB = 1.0f / (float)r.B;
+    const float lo = 1.0f - r.eps_clip, hi = 1.0f + r.eps_clip;
+    const int hr = RPW * w + min(lane, RPW - 1);  // this lane's row (lanes >= RPW: a copy)
+    f32x4 dsum = HDOT[0][hr];
+#pragma unroll
+    for (int ww = 1; ww < NW; ++ww) dsum += HDOT[ww][hr];
+    const float mu0 = dsum[0] + ba0, mu1 = dsum[1] + ba1, val = dsum[2] + bcv;
+    const float d0 = hz0 - mu0, d1 = hz1 - mu1;
+    const float t0 = tanhf(hz0), t1 = tanhf(hz1);
+    const float lp0 = -(d0 * d0) / (2.0f * var0) - lsc0 - LOG_SQRT_2PI;
+    const float lp1 = -(d1 * d1) / (2.0f * var1) - lsc1 - LOG_SQRT_2PI;
+    const float logp = (lp0 - log1pf(-(t0 * t0) + 1e-6f)) + (lp1 - log1pf(-(t1 * t1) + 1e-6f));
+    const float log_ratio = logp - hold;
+    const float ratio = expf(log_ratio);
+    const float cr = fminf(fmaxf(ratio, lo), hi);
+    const float s1 = ratio * hadv, s2 = cr * hadv;
+    const float inr = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
+    // torch.min / clamp backward: ties split the gradient evenly
+    const float wsel = s1 < s2 ? 1.0f : (s1 > s2 ? inr : 0.5f * (1.0f + inr));
+    const float dlogp = -invB * hadv * wsel * ratio;  // d(actor_loss)/d(logp)
+    // rows past nrows (and lanes past RPW) contribute nothing
+    const bool live = lane < RPW && hr < nrows;
+    const float dmu0 = live ? dlogp * d0 / var0 : 0.0f;
+    const float dmu1 = live ? dlogp * d1 / var1 : 0.0f;
+    const float dv = live ? r.value_coef * 2.0f * (val - hret) * invB : 0.0f;
+    if (lane < RPW) HROW[hr] = f32x4{dmu0, dmu1, dv, 0.0f};
+    // this wave's rows' bias / log_std gradient terms and metrics, summed over its lanes in
+    // lane order (the quad / half-row / row DPP tree over RPW <= 16 lanes)
+    float tl[9] = {dmu0, dmu1, dv,
+                   live ? dlogp * ((d0 * d0) / var0 - 1.0f) : 0.0f,
+                   live ? dlogp * ((d1 * d1) / var1 - 1.0f) : 0.0f,
+                   live ? -fminf(s1, s2) : 0.0f,
+                   live ? (val - hret) * (val - hret) : 0.0f,
+                   live ? (fabsf(ratio - 1.0f) > r.eps_clip ? 1.0f : 0.0f) : 0.0f,
+                   live ? (ratio - 1.0f) - log_ratio : 0.0f};
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const float v = row16_sum(lane < 16 ? tl[k] : 0.0f);
+      if (lane == 0) HTAIL[w][k] = v;
     }
-    float wa0[QH], wa1[QH], wc[QH];
-  #pragma unroll
-    for (int q = 0; q < QH; ++q) {
-      const int col = lane + 64 * q;
-      wa0[q] = P[r.off[P_WA2] + col];
-      wa1[q] = P[r.off[P_WA2] + H + col];
-      wc[q] = P[r.off[P_WC2] + col];
-    }
-    const float ba0 = P[r.off[P_BA2]], ba1 = P[r.off[P_BA2] + 1], bcv = P[r.off[P_BC2]];
-    const float ls0 = P[r.off[P_LOGSTD]], ls1 = P[r.off[P_LOGSTD] + 1];
-    f32x4 unused_a[RB][TW], unused_c[RB][TW];
-    rows_forward<QH, NW, RT, false>(R, r.states, r.idx, S, nrows, row0, P, r.off, X, H1, H2, AC,
-                                    r.xg, r.h1, r.h2, unused_a, unused_c PSEC_ARGS);
-    PSEC(3);
-
-    // ---- loss head (ppo/agent.py:226-245): wave w takes rows RPW*w ..; lane owns the hidden
-    // columns lane + 64q; dL/d[a1|c1] overwrites [a1|c1] in LDS (and goes to HBM for ppo_wgrad);
-    // the head weight / bias / log_std gradients stay in registers until the waves combine them
-    float ga0[QH], ga1[QH], gc[QH];
-    float s_dba0 = 0, s_dba1 = 0, s_dbc = 0, s_dls0 = 0, s_dls1 = 0;
-    float s_pg = 0, s_vf = 0, s_clip = 0, s_kl = 0;
-    {
-  #pragma unroll
-      for (int q = 0; q < QH; ++q) ga0[q] = ga1[q] = gc[q] = 0.0f;
-      // torch Normal: scale = exp(log_std); var = scale**2; log_scale = log(scale)
-      const float sc0 = expf(ls0), sc1 = expf(ls1);
-      const float var0 = sc0 * sc0, var1 = sc1 * sc1;
-      const float lsc0 = logf(sc0), lsc1 = logf(sc1);
-      const float LOG_SQRT_2PI = 0.91893853320467274178f;
-      const float invB = 1.0f / (float)r.B;
-      const float lo = 1.0f - r.eps_clip, hi = 1.0f + r.eps_clip;
-      // the heads' dot products of all this wave's rows first, so that their reductions overlap
-      float hmu0[RPW], hmu1[RPW], hval[RPW];
-  #pragma unroll
-      for (int rr = 0; rr < RPW; ++rr) {
-        const float* arow = AC + min(RPW * w + rr, nrows - 1) * PA;
-        float p0 = 0.0f, p1 = 0.0f, pv = 0.0f;
-  #pragma unroll
-        for (int q = 0; q < QH; ++q) {
-          const int col = lane + 64 * q;
-          const float av = arow[col], cv = arow[H + col];
-          p0 += av * wa0[q];
-          p1 += av * wa1[q];
-          pv += cv * wc[q];
-        }
-        hmu0[rr] = wave_sum_dpp(p0) + ba0;
-        hmu1[rr] = wave_sum_dpp(p1) + ba1;
-        hval[rr] = wave_sum_dpp(pv) + bcv;
-      }
-      PSEC(7);
-      // the per-row scalar part once for all this wave's rows: row rr on lane rr
-      float c_dmu0, c_dmu1, c_dv, c_dls0, c_dls1, c_pg, c_vf, c_clip, c_kl;
-      {
-        const int rs = min(lane, RPW - 1);
-        float z0 = hz0[0], z1 = hz1[0], old = hold[0], ad = hadv[0], rt = hret[0];
-        float mu0 = hmu0[0], mu1 = hmu1[0], val = hval[0];
-  #pragma unroll
-        for (int rr = 1; rr < RPW; ++rr)
-          if (rs == rr) {
-            z0 = hz0[rr], z1 = hz1[rr], old = hold[rr], ad = hadv[rr], rt = hret[rr];
-            mu0 = hmu0[rr], mu1 = hmu1[rr], val = hval[rr];
-          }
-        const float d0 = z0 - mu0, d1 = z1 - mu1;
-        const float t0 = tanhf(z0), t1 = tanhf(z1);
-        const float lp0 = -(d0 * d0) / (2.0f * var0) - lsc0 - LOG_SQRT_2PI;
-        const float lp1 = -(d1 * d1) / (2.0f * var1) - lsc1 - LOG_SQRT_2PI;
-        const float logp =
-            (lp0 - log1pf(-(t0 * t0) + 1e-6f)) + (lp1 - log1pf(-(t1 * t1) + 1e-6f));
-        const float log_ratio = logp - old;
-        const float ratio = expf(log_ratio);
-        const float cr = fminf(fmaxf(ratio, lo), hi);
-        const float s1 = ratio * ad, s2 = cr * ad;
-        const float inr = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
-        // torch.min / clamp backward: ties split the gradient evenly
-        const float wsel = s1 < s2 ? 1.0f : (s1 > s2 ? inr : 0.5f * (1.0f + inr));
-        const float dlogp = -invB * ad * wsel * ratio;  // d(actor_loss)/d(logp)
-        c_dmu0 = dlogp * d0 / var0;
-        c_dmu1 = dlogp * d1 / var1;
-        c_dv = r.value_coef * 2.0f * (val - rt) * invB;
-        c_dls0 = dlogp * ((d0 * d0) / var0 - 1.0f);
-        c_dls1 = dlogp * ((d1 * d1) / var1 - 1.0f);
-        c_pg = -fminf(s1, s2);
-        c_vf = (val - rt) * (val - rt);
-        c_clip = fabsf(ratio - 1.0f) > r.eps_clip ? 1.0f : 0.0f;
-        c_kl = (ratio - 1.0f) - log_ratio;
-      }
-      auto lane_f = [](float v, int l) {
-        return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
-      };
-  #pragma unroll
-      for (int rr = 0; rr < RPW; ++rr) {
-        const int lr = RPW * w + rr;
-        if (lr >= nrows) break;
-        float* arow = AC + lr * PA;
-        const float dmu0 = lane_f(c_dmu0, rr), dmu1 = lane_f(c_dmu1, rr), dv = lane_f(c_dv, rr);
-  #pragma unroll
-        for (int q = 0; q < QH; ++q) {
-          const int col = lane + 64 * q;
-          const float a = arow[col], cc = arow[H + col];
-          const float da = a > 0.0f ? (dmu0 * wa0[q] + dmu1 * wa1[q]) : 0.0f;
-          const float dc = cc > 0.0f ? dv * wc[q] : 0.0f;
-          arow[col] = da;  // dac: the image is copied to HBM whole after the barrier
-          arow[H + col] = dc;
-          ga0[q] += dmu0 * a;
-          ga1[q] += dmu1 * a;
-          gc[q] += dv * cc;
-        }
-        s_dba0 += dmu0;
-        s_dba1 += dmu1;
-        s_dbc += dv;
-        s_dls0 += lane_f(c_dls0, rr);
-        s_dls1 += lane_f(c_dls1, rr);
-        s_pg += lane_f(c_pg, rr);
-        s_vf += lane_f(c_vf, rr);
-        s_clip += lane_f(c_clip, rr);
-        s_kl += lane_f(c_kl, rr);
-      }
-      PSEC(11);
-      if (blockIdx.x == 0 && t == 0) {
-        r.counters[0] += 1;  // Adam step t for this minibatch
-        r.counters[1] += 1;  // metrics row (this step writes row counters[1]-1)
-      }
-    }
-    __syncthreads();
-    rows_out<NT, RT>(AC, PA, r.dac + (long)row0 * 2 * H, 2 * H, 2 * H, nrows);
-    PSEC(4);
-    // dh2 = (dac [Wa1; Wc1]) * (h2 > 0)   ([Wa1; Wc1] is [2H][H]: k-major); the two halves of
-    // K = 2H (Wa1 rows, Wc1 rows) are summed at the end
-    zero_acc(acc);
-    R.template run<4>(AC, PA, acc);
-    R.template run<5>(AC + H, PA, acc);
-    row_epi_mask(acc, H2, PH, nb);
-    __syncthreads();
-    if (r.dh2) rows_out<NT, RT>(H2, PH, r.dh2 + (long)row0 * H, H, H, nrows);
-    PSEC(5);
-    // the head partials of the NW waves -> one row per workgroup (fixed order); [a1|c1] is free
-    {
-      float* wp = HPW + w * WPS;
-  #pragma unroll
-      for (int q = 0; q < QH; ++q) {
-        const int col = lane + 64 * q;
-        wp[col] = ga0[q];
-        wp[H + col] = ga1[q];
-        wp[2 * H + col] = gc[q];
-      }
-      if (lane == 0) {
-        float* tl = wp + 3 * H;
-        tl[0] = s_dba0, tl[1] = s_dba1, tl[2] = s_dbc, tl[3] = s_dls0, tl[4] = s_dls1;
-        tl[5] = s_pg, tl[6] = s_vf, tl[7] = s_clip, tl[8] = s_kl;
-      }
-      __syncthreads();
-      float* out = r.head_part + (long)blockIdx.x * r.HP;
-      for (int j = t; j < 3 * H + 9; j += NT) {
-        float v = HPW[j];
-  #pragma unroll
-        for (int ww = 1; ww < NW; ++ww) v += HPW[ww * WPS + j];
-        out[j] = v;
-      }
+    if (blockIdx.x == 0 && t == 0) {
+      r.counters[0] += 1;  // Adam step t for this minibatch
+      r.counters[1] += 1;  // metrics row (this step writes row counters[1]-1)
     }
   }
+  __syncthreads();
+  PSEC(11);
+  {
+    // dac of this wave's columns (the reference's expression per element), and the head
+    // weight gradients sum_rows dmu * a1 / dv * c1 of its columns: per lane over its rows, then
+    // over the four 16-lane groups
+    float ga0[TW], ga1[TW], gc[TW];
+#pragma unroll
+    for (int u = 0; u < TW; ++u) ga0[u] = ga1[u] = gc[u] = 0.0f;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 16 * rb + 4 * g4 + q;
+        const f32x4 sc = HROW[row];
+        const float dmu0 = sc[0], dmu1 = sc[1], dv = sc[2];
+        float* arow = AC + row * PA;
+#pragma unroll
+        for (int u = 0; u < TW; ++u) {
+          const int col = nb + 16 * u + c16;
+          const float a = av[rb][u][q], cc = cv[rb][u][q];
+          arow[col] = a > 0.0f ? (dmu0 * wa0[u] + dmu1 * wa1[u]) : 0.0f;
+          arow[H + col] = cc > 0.0f ? dv * wc[u] : 0.0f;
+          ga0[u] += dmu0 * a;
+          ga1[u] += dmu1 * a;
+          gc[u] += dv * cc;
+        }
+      }
+    float* out = r.head_part + (long)blockIdx.x * r.HP;
+#pragma unroll
+    for (int u = 0; u < TW; ++u) {
+      // lanes c, c+16, c+32, c+48 hold the same column: (g0 + g1) + (g2 + g3)
+      ga0[u] += __shfl_xor(ga0[u], 16);
+      ga1[u] += __shfl_xor(ga1[u], 16);
+      gc[u] += __shfl_xor(gc[u], 16);
+      ga0[u] += __shfl_xor(ga0[u], 32);
+      ga1[u] += __shfl_xor(ga1[u], 32);
+      gc[u] += __shfl_xor(gc[u], 32);
+      if (g4 == 0) {
+        const int col = nb + 16 * u + c16;
+        out[col] = ga0[u];
+        out[H + col] = ga1[u];
+        out[2 * H + col] = gc[u];
+      }
+    }
+    if (w == 0 && lane < 9) {  // the waves' tail sums in wave order
+      float v = HTAIL[0][lane];
+#pragma unroll
+      for (int ww = 1; ww < NW; ++ww) v += HTAIL[ww][lane];
+      out[3 * H + lane] = v;
+    }
+  }
+  __syncthreads();
+  rows_out<NT, RT>(AC, PA, r.dac + (long)row0 * 2 * H, 2 * H, 2 * H, nrows);
+  PSEC(4);
+  // dh2 = (dac [Wa1; Wc1]) * (h2 > 0)   ([Wa1; Wc1] is [2H][H]: k-major); the two halves of
+  // K = 2H (Wa1 rows, Wc1 rows) are summed at the end
+  zero_acc(acc);
+  R.template run<4>(AC, PA, acc);
+  R.template run<5>(AC + H, PA, acc);
+  row_epi_mask(acc, H2, PH, nb);
+  __syncthreads();
+  if (r.dh2) rows_out<NT, RT>(H2, PH, r.dh2 + (long)row0 * H, H, H, nrows);
+  PSEC(5);
   // dh1 = (dh2 W2) * (h1 > 0)
   zero_acc(acc);
   R.template run<6>(H2, PH, acc);
