@@ -489,15 +489,17 @@ inline Work carve(const hwy_ppo_dims& d, void* ws, int64_t* bytes_out) {
   // each, at most 8 (one per XCD)
   w.split = std::max(1, std::min({8, 256 / ntile, (B + 63) / 64}));
   w.grid2 = ntile * w.split + w.nh;
-  // balanced partition (ppo_wgrad): 32 workgroups per slice when 16-30 tiles leave CUs idle
-  // and the slices are long enough to split; an extra pays ~1.5 chunks of pipeline fill per tile
+  // balanced partition (ppo_wgrad): 256 / split workgroups per slice when the tiles leave at
+  // least two CUs of each slice's share idle and the slices are long enough to split; an extra
+  // pays ~1.5 chunks of pipeline fill per tile
   w.bal = 0, w.wm = 0, w.tpe = 0, w.nslot = 1;
   {
-    const int nck = ((B + 7) / 8 + 63) / 64;  // chunks of the longest slice
-    if (wg_balance_on() && w.split == 8 && ntile >= 16 && ntile <= 30 && nck >= 16) {
-      const int E = 32 - ntile, tpe = (ntile + E - 1) / E;
+    const int P = 256 / w.split;                               // workgroups per slice
+    const int nck = ((B + w.split - 1) / w.split + 63) / 64;  // chunks of the longest slice
+    if (wg_balance_on() && ntile >= 16 && P - ntile >= 2 && nck >= 16) {
+      const int E = P - ntile, tpe = (ntile + E - 1) / E;
       const int m = (int)std::ceil(tpe * (nck + 1.5) / (1.0 + tpe));
-      if (m < nck) w.bal = 1, w.wm = m, w.tpe = tpe, w.nslot = 2, w.grid2 = 8 * 32;
+      if (m < nck) w.bal = 1, w.wm = m, w.tpe = tpe, w.nslot = 2, w.grid2 = w.split * P;
     }
   }
   w.nred2 = w.nh + ntile * (kWgTM * kWgTN / 1024);
@@ -1639,11 +1641,12 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int tile_id, int kb0
 // ...)), then the head-sum workgroups.  Slice z goes to workgroups with id % 8 = z, i.e. to one
 // XCD (the dispatcher deals workgroups to the 8 XCDs round-robin), so each XCD reads one slice
 // of the activations and serves all its tiles from its own L2.
-// Balanced (a.bal; 26 tiles x 8 slices would leave 48 of 256 CUs idle): 32 workgroups per
-// slice.  Workgroup j < ntile takes tile j over the slice's first wm chunks, in lockstep with
-// the other tiles (the XCD's L2 holds the chunks they share); the 32 - ntile "extras" take the
-// remaining chunks of tpe tiles each (those chunks stay L2-resident while an extra walks its
-// tiles), into a second partial slot; the last extra of each slice also runs the head sums.
+// Balanced (a.bal; e.g. 26 tiles x 8 slices would leave 48 of 256 CUs idle): 256 / split
+// workgroups per slice.  Workgroup j < ntile takes tile j over the slice's first wm chunks, in
+// lockstep with the other tiles (the XCD's L2 holds the chunks they share); the remaining
+// 256 / split - ntile "extras" take the other chunks of tpe tiles each (those chunks stay
+// L2-resident while an extra walks its tiles), into a second partial slot; the last extra of
+// each slice also runs the head sums.
 __global__ void __launch_bounds__(512) ppo_wgrad(WgArgs a) {
   PSEC_DECL
   __shared__ __attribute__((aligned(16))) float wg_lds[2 * (kWgTM + kWgTN) * 64];
@@ -1673,7 +1676,7 @@ __global__ void __launch_bounds__(512) ppo_wgrad(WgArgs a) {
   if (j < ntile) {
     wgrad_tile(a, j, kz, km, slot(j, 0), wg_lds PSEC_ARGS);
   } else {
-    const int e = j - ntile, nextra = 32 - ntile;
+    const int e = j - ntile, nextra = (int)gridDim.x / a.split - ntile;
     const int t0 = min(ntile, e * a.tpe), t1 = min(ntile, t0 + a.tpe);
     for (int tile = t0; tile < t1; ++tile) {
       if (tile > t0) __syncthreads();  // the last segment's accumulator exchange used the LDS
