@@ -498,7 +498,11 @@ inline Work carve(const hwy_ppo_dims& d, void* ws, int64_t* bytes_out) {
     const int nck = ((B + w.split - 1) / w.split + 63) / 64;  // chunks of the longest slice
     if (wg_balance_on() && ntile >= 16 && P - ntile >= 2 && nck >= 16) {
       const int E = P - ntile, tpe = (ntile + E - 1) / E;
-      const int m = (int)std::ceil(tpe * (nck + 1.5) / (1.0 + tpe));
+      static const double fill = [] {  // HWY_WG_FILL: development A/B of the fill price
+        const char* e = getenv("HWY_WG_FILL");
+        return e ? atof(e) : 1.5;
+      }();
+      const int m = (int)std::ceil(tpe * (nck + fill) / (1.0 + tpe));
       if (m < nck) w.bal = 1, w.wm = m, w.tpe = tpe, w.nslot = 2, w.grid2 = w.split * P;
     }
   }
