@@ -1251,6 +1251,9 @@ struct ActArgs {
   const float* tiles;  // weight tile image in step with params (TL), else null
 };
 
+#ifndef HWY_ACT_NW
+#define HWY_ACT_NW 8  // waves of ppo_act at H = 256 (development A/B)
+#endif
 template <int QH, int NW, bool TL>
 __global__ void __launch_bounds__(64 * NW, 1) ppo_act(ActArgs r) {
   constexpr int H = 64 * QH;
@@ -2291,7 +2294,7 @@ int hwy_ppo_act(const hwy_ppo_act_args* a, void* stream) {
       case 1: hipLaunchKernelGGL((ppo_act<1, 4, TL>), g, b4, 0, s, r); break;
       case 2: hipLaunchKernelGGL((ppo_act<2, 8, TL>), g, b8, 0, s, r); break;
       case 3: hipLaunchKernelGGL((ppo_act<3, 4, TL>), g, b4, 0, s, r); break;
-      case 4: hipLaunchKernelGGL((ppo_act<4, 8, TL>), g, b8, 0, s, r); break;
+      case 4: hipLaunchKernelGGL((ppo_act<4, HWY_ACT_NW, TL>), g, dim3(64 * HWY_ACT_NW), 0, s, r); break;
       case 5: hipLaunchKernelGGL((ppo_act<5, 4, TL>), g, b4, 0, s, r); break;
       case 6: hipLaunchKernelGGL((ppo_act<6, 8, TL>), g, b8, 0, s, r); break;
       case 7: hipLaunchKernelGGL((ppo_act<7, 4, TL>), g, b4, 0, s, r); break;

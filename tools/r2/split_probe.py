@@ -13,6 +13,10 @@ sys.path.insert(0, os.path.join(ROOT, "highway-rope-ppo_amd"))
 
 import torch  # noqa: E402
 
+from hwy import native  # noqa: E402
+
+if os.environ.get("HWY_LIB"):  # a variant library (development A/B)
+    native.LIB_PATH = os.environ["HWY_LIB"]
 from config.base_config import HIGHWAY_CONFIG  # noqa: E402
 from experiments.config import Condition  # noqa: E402
 from experiments.wrappers import make_env  # noqa: E402
@@ -64,6 +68,8 @@ def timeit(fn):
 
 
 print(f"single stream graph, E={E}: {timeit(roll.run):.3f} ms per rollout of {T}")
+if os.environ.get("SPLIT", "1") == "0":
+    sys.exit(0)
 
 # two halves, each its own chain, captured into one graph on two streams
 for _, b, _ in halves:
