@@ -426,27 +426,64 @@ struct Work {
   int sb, hb;  // ring blocks of the row kernels (rows_blocks)
 };
 
-// ppo_wgrad's balanced partition (see ppo_wgrad); HWY_WG_BAL=0 keeps one workgroup per
-// (tile, slice) (development A/B)
-inline bool wg_balance_on() {
-  static const bool on = [] {
-    const char* e = getenv("HWY_WG_BAL");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
+// The chip the partitions are sized for: compute units and XCDs of the current device
+// (hipDeviceAttributeNumberOfXccs; a compute-partitioned MI355X reports its own share).  Without
+// a device (the CPU-side workspace queries of the tests) the full MI355X: 256 CUs, 8 XCDs.
+struct ChipGeom {
+  int cus, xcds;
+};
+inline ChipGeom chip_geom() {
+  static ChipGeom cache[64];
+  static bool have[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    (void)hipGetLastError();
+    return {256, 8};
+  }
+  if (!have[dev]) {
+    int cus = 0, xcds = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus < 1)
+      cus = 256;
+    if (hipDeviceGetAttribute(&xcds, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess ||
+        xcds < 1 || xcds > cus)
+      xcds = 1;
+    (void)hipGetLastError();
+    cache[dev] = {cus, xcds};
+    have[dev] = true;
+  }
+  return cache[dev];
 }
+
+// Development knobs (make dev builds only, -DHWY_DEV_KNOBS): HWY_WG_BAL=0 keeps one ppo_wgrad
+// workgroup per (tile, slice), HWY_ROWS_RT=16|32 forces the ppo_rows tile, HWY_WG_FILL prices an
+// extra's pipeline fill.  The product library reads no environment: the partitions, and with
+// them the summation order of every gradient, depend only on the shapes and the chip.
+#ifdef HWY_DEV_KNOBS
+inline int dev_knob_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+inline double dev_knob_double(const char* name, double dflt) {
+  const char* e = getenv(name);
+  return e ? atof(e) : dflt;
+}
+#else
+inline int dev_knob_int(const char*, int dflt) { return dflt; }
+inline double dev_knob_double(const char*, double dflt) { return dflt; }
+#endif
+
+// ppo_wgrad's balanced partition (see ppo_wgrad)
+inline bool wg_balance_on() { return dev_knob_int("HWY_WG_BAL", 1) != 0; }
 
 // minibatch rows per ppo_rows workgroup: 32 (two 16-row blocks sharing every weight register
 // block: half the weight stream per row) when the grid still covers the chip and the LDS images
-// fit (H <= 256), else 16.  HWY_ROWS_RT=16|32 forces one (development A/B).
+// fit (H <= 256), else 16.
 inline int rows_tile(int B, int H) {
-  static const int force = [] {
-    const char* e = getenv("HWY_ROWS_RT");
-    return e ? atoi(e) : 0;
-  }();
   if (H > 256) return kRowTile;
+  const int force = dev_knob_int("HWY_ROWS_RT", 0);
   if (force == 16 || force == 32) return force;
-  return B >= 8192 ? 2 * kRowTile : kRowTile;
+  return B >= 32 * chip_geom().cus ? 2 * kRowTile : kRowTile;
 }
 
 // the fused row path covers the reference's shapes: float4 state rows, H a multiple of 64
@@ -485,23 +522,30 @@ inline Work carve(const hwy_ppo_dims& d, void* ws, int64_t* bytes_out) {
   w.t1 = tmh * ((S + kWgTN - 1) / kWgTN);
   w.nh = (3 * H + 9 + 63) / 64;
   const int ntile = w.tac + w.t2 + w.t1;
-  // row slices per tile: one workgroup per CU (~256 on the chip), at least one 64-row chunk
-  // each, at most 8 (one per XCD)
-  w.split = std::max(1, std::min({8, 256 / ntile, (B + 63) / 64}));
+  // row slices per tile: one workgroup per CU, at least one 64-row chunk each, at most one per
+  // XCD, and a divisor of the XCD count (slice z = workgroup id % split then lands on the XCDs
+  // x with x % split == z under the dispatcher's round-robin placement -- for L2 locality only)
+  const ChipGeom chip = chip_geom();
+  {
+    const int cap = std::max(1, std::min({chip.xcds, 8, chip.cus / ntile, (B + 63) / 64}));
+    w.split = 1;
+    for (int sp = cap; sp >= 1; --sp)
+      if (chip.xcds % sp == 0) {
+        w.split = sp;
+        break;
+      }
+  }
   w.grid2 = ntile * w.split + w.nh;
-  // balanced partition (ppo_wgrad): 256 / split workgroups per slice when the tiles leave at
+  // balanced partition (ppo_wgrad): cus / split workgroups per slice when the tiles leave at
   // least two CUs of each slice's share idle and the slices are long enough to split; an extra
   // pays ~1.5 chunks of pipeline fill per tile
   w.bal = 0, w.wm = 0, w.tpe = 0, w.nslot = 1;
   {
-    const int P = 256 / w.split;                               // workgroups per slice
+    const int P = chip.cus / w.split;                          // workgroups per slice
     const int nck = ((B + w.split - 1) / w.split + 63) / 64;  // chunks of the longest slice
     if (wg_balance_on() && ntile >= 16 && P - ntile >= 2 && nck >= 16) {
       const int E = P - ntile, tpe = (ntile + E - 1) / E;
-      static const double fill = [] {  // HWY_WG_FILL: development A/B of the fill price
-        const char* e = getenv("HWY_WG_FILL");
-        return e ? atof(e) : 1.5;
-      }();
+      const double fill = dev_knob_double("HWY_WG_FILL", 1.5);
       const int m = (int)std::ceil(tpe * (nck + fill) / (1.0 + tpe));
       if (m < nck) w.bal = 1, w.wm = m, w.tpe = tpe, w.nslot = 2, w.grid2 = w.split * P;
     }
@@ -2306,6 +2350,17 @@ int hwy_ppo_act(const hwy_ppo_act_args* a, void* stream) {
   else
     launch(std::integral_constant<bool, false>());
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int hwy_ppo_build_flags(void) {
+  int f = 0;
+#ifdef HWY_DEV_KNOBS
+  f |= 1;
+#endif
+#ifdef HWY_SECTION_PROFILE
+  f |= 2;
+#endif
+  return f;
 }
 
 #ifdef HWY_SECTION_PROFILE

@@ -116,7 +116,7 @@ def flat_params(agent):
             p.grad = grads[off:off + n].view_as(p)
             params.append(p)
     agent._flat = (flat, grads, offs, params)
-    agent._learner = None  # a torch-graph learner captured the old storage
+    agent._learners = {}  # a torch-graph learner captured the old storage
     return agent._flat
 
 
@@ -306,6 +306,16 @@ class FusedPPO:
     def run(self, states, pre_tanh, old_lp, adv, ret, perm: torch.Tensor) -> torch.Tensor:
         """All epochs of one update; returns the [epochs*nmb, 6] metrics rows (device)."""
         mb, nmb, epochs = self.mb, self.nmb, self.agent.epochs
+        # Adam's state moves here if the agent's torch optimizer stepped last (ppo/agent.py);
+        # an instance not (yet) registered as agent._fused takes the state over the same way
+        ag = self.agent
+        if hasattr(ag, "_adam_to") and getattr(ag, "_fused", None) in (None, self):
+            if ag._fused is self:
+                ag._adam_to("fused")
+            else:
+                if ag._adam_owner != "fused":
+                    self._import_torch_state()
+                ag._adam_owner = "fused"
         # the captured graphs bake in the buffer addresses and the scalar hyper-parameters of
         # PpoArgs: a change to either (an lr schedule, agent.eps_clip, ...) forces a recapture
         key = (states.data_ptr(), pre_tanh.data_ptr(), old_lp.data_ptr(), adv.data_ptr(),

@@ -228,6 +228,17 @@ class _Learner:
         self.use_graph = use_graph and dev.type == "cuda"
         self.g_fwd = self.g_opt = None
 
+    def activate(self):
+        """Point every parameter's .grad at this learner's flat buffer (another cached learner,
+        or FusedPPO's flat gradient, may hold them); the same views, so captured graphs stay
+        valid."""
+        p0 = self.params[0]
+        if p0.grad is None or p0.grad.data_ptr() != self.flat_grad.data_ptr():
+            off = 0
+            for p in self.params:
+                p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
+                off += p.numel()
+
     def bind(self, states, pre_tanh, old_logp, adv, ret):
         same = all(self.src.get(k) is v for k, v in (("s", states), ("z", pre_tanh),
                                                       ("lp", old_logp), ("a", adv), ("r", ret)))
@@ -386,7 +397,13 @@ class PPOAgent:
         self.use_graphs = use_graphs
         self.logger = logger or logging.getLogger(__name__)
         self.memory = PPOMemory(batch_size=batch_size, device=self.device)
-        self._learner: Optional[_Learner] = None
+        # torch-path learners, one per (rows, minibatch, steps, graph) geometry: a ragged
+        # partition alternates between two sizes without reallocating
+        self._learners: Dict[tuple, _Learner] = {}
+        # which optimizer holds the current Adam state: "torch" (agent.optimizer) or "fused"
+        # (FusedPPO's m / v / step); handed over whenever an update switches paths
+        self._adam_owner = "torch"
+        self._warned_ragged = False
         self.updates = 0  # completed update() / update_rollout() calls (evaluation memo key)
         self.generator = None
         if self.device.type == "cuda":
@@ -457,13 +474,28 @@ class PPOAgent:
         return pending if deferred else pending.result()
 
     def _learner_for(self, n: int, mb: int, steps: int, graph: bool) -> _Learner:
-        L = self._learner
-        if L is None or L.n != n or L.mb != mb or L.metrics.shape[0] != steps:
+        key = (n, mb, steps, graph)
+        L = self._learners.get(key)
+        if L is None:
             L = _Learner(self, n, mb, steps, graph, group=self._dist)
-            self._learner = L
+            self._learners[key] = L
+        L.activate()
         return L
 
+    def _adam_to(self, owner: str):
+        """Hand the Adam state (moments, step count) to the optimizer about to step."""
+        if owner == self._adam_owner:
+            return
+        F = self._fused
+        if F is not None:
+            if owner == "torch":
+                F.export_torch_state()
+            else:
+                F._import_torch_state()
+        self._adam_owner = owner
+
     def _run_epochs(self, states, pre_tanh, old_logp, adv, ret, batches: List[torch.Tensor]):
+        self._adam_to("torch")
         n = states.shape[0]
         sizes = {int(b.numel()) for b in batches}
         mb = max(sizes)
@@ -540,6 +572,7 @@ class PPOAgent:
         mb, nmb = sizes[0], len(sizes)
         if len(set(sizes)) == 1 and self._fused_ok(mb):
             F = self._fused_for(mb, nmb, n)
+            self._adam_to("fused")
             F_adv, F_ret, F_perm = self._static_bufs
             F_adv.copy_(adv)
             F_ret.copy_(ret)
@@ -548,6 +581,12 @@ class PPOAgent:
         else:
             # one partition for all epochs (ppo/agent.py:205); a short last minibatch takes the
             # reference's ragged path (eager torch steps at the exact sizes)
+            if len(set(sizes)) > 1 and not self._warned_ragged and self._fused_ok(mb):
+                self._warned_ragged = True
+                self.logger.warning(
+                    f"update_rollout: {n} samples split into unequal minibatches {sorted(set(sizes))}"
+                    " -- the fused HIP update needs equal sizes, so these updates run the eager "
+                    "torch path (choose num_minibatches / batch_size dividing T x E)")
             starts = np.cumsum([0] + sizes)
             batches = [perm[int(starts[i]):int(starts[i + 1])] for i in range(nmb)]
             rows = self._run_epochs(states, pre_tanh, old_lp, adv, ret, batches)
@@ -589,11 +628,12 @@ class PPOAgent:
 
         F = self._fused
         if F is None or F.mb != mb or F.nmb != nmb or F.metrics.shape[0] != self.epochs * nmb:
-            if F is not None:  # carry Adam's moments and step count over to the new instance
-                F.export_torch_state()
+            if F is not None and self._adam_owner == "fused":
+                F.export_torch_state()  # carry Adam's moments and step count to the new instance
+            self._adam_owner = "torch"  # the new instance imports agent.optimizer's state
             F = FusedPPO(self, mb, nmb, group=self._dist, use_graphs=self.use_graphs)
             self._fused = F
-            self._learner = None
+            self._learners = {}
         bufs = getattr(self, "_static_bufs", None)
         if bufs is None or bufs[0].numel() != n:
             dev = self.device
@@ -603,7 +643,7 @@ class PPOAgent:
 
     # ------------------------------------------------------------------ checkpoints
     def save(self, path: str):
-        if self._fused is not None:
+        if self._fused is not None and self._adam_owner == "fused":
             self._fused.export_torch_state()
         torch.save({"model": self.actor_critic.state_dict(),
                     "optimizer": self.optimizer.state_dict()}, path)
@@ -614,8 +654,8 @@ class PPOAgent:
         self.actor_critic.load_state_dict(ckpt["model"])
         if load_optimizer and "optimizer" in ckpt:
             self.optimizer.load_state_dict(ckpt["optimizer"])
-            if self._fused is not None:
+            if self._fused is not None and self._adam_owner == "fused":
                 self._fused._import_torch_state()
-        self._learner = None
+        self._learners = {}
         self.logger.info(f"model_loaded path={path}")
         return ckpt.get("config", {})

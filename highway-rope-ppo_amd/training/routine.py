@@ -80,7 +80,11 @@ def _eval_key(agent, num_episodes, exp_seed):
     """Identity of a deterministic evaluation: the same weights (no update since, no torch-side
     parameter write) on the same seeds give the same return, bit for bit."""
     params = tuple((p.data_ptr(), p._version) for p in agent.actor_critic.parameters())
-    return (getattr(agent, "updates", None), params, num_episodes, exp_seed)
+    # on the fused path every p.data is a view of one flat buffer: writes through that buffer
+    # (the fused optimizer, a copy into it) bump only the buffer's counter (ADVICE r2)
+    flat = getattr(agent, "_flat", None)
+    flat_v = (flat[0].data_ptr(), flat[0]._version) if flat is not None else None
+    return (getattr(agent, "updates", None), params, flat_v, num_episodes, exp_seed)
 
 
 def _evaluate_vector(env, agent, num_episodes, exp_seed):

@@ -100,6 +100,11 @@ typedef struct hwy_ppo_act_args {
 } hwy_ppo_act_args;
 int hwy_ppo_act(const hwy_ppo_act_args* a, void* stream);
 
+/* Build flags of this library: bit 0 = development knobs compiled in (HWY_DEV_KNOBS: the
+ * HWY_WG_BAL / HWY_ROWS_RT / HWY_WG_FILL environment variables are read), bit 1 = section clocks
+ * (HWY_SECTION_PROFILE).  A product build returns 0 and reads no environment variable. */
+int hwy_ppo_build_flags(void);
+
 #ifdef __cplusplus
 }
 #endif

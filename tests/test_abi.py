@@ -97,3 +97,16 @@ def test_ppo_param_layout_matches_actor_critic():
         assert numel == sum(sizes) == sum(p.numel() for p in ac.parameters())
     with pytest.raises(ValueError):
         param_layout(60, 100)  # hidden_dim not a multiple of 64
+
+
+def test_product_library_reads_no_development_knobs(lib):
+    """The shipped libhwy.so is a product build: the development knobs that change the PPO
+    partitions (HWY_WG_BAL / HWY_ROWS_RT / HWY_WG_FILL) and the section clocks are compiled out
+    (hwy_ppo_build_flags() == 0), so no environment variable changes a gradient's summation
+    order."""
+    lib.hwy_ppo_build_flags.restype = ctypes.c_int
+    assert lib.hwy_ppo_build_flags() == 0
+    src = open(os.path.join(ROOT, "highway-rope-ppo_amd", "csrc", "ppo_kernels.hip")).read()
+    # every getenv of the PPO kernels sits inside the HWY_DEV_KNOBS block
+    dev = src[src.index("#ifdef HWY_DEV_KNOBS"):src.index("#endif", src.index("#ifdef HWY_DEV_KNOBS"))]
+    assert src.count("getenv(") == dev.count("getenv(")

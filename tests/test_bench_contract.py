@@ -56,3 +56,12 @@ def test_cpu_share_is_bounded_by_the_machine():
     b = _bench()
     c = b.cpu_share()
     assert 1 <= c["share"] <= c["os_cpu_count"] and c["affinity"] <= c["os_cpu_count"]
+
+
+def test_metric_string_is_baselines():
+    """configs[1]'s line carries BASELINE.json's metric verbatim; other configs name their own
+    workload (no 4096 x 15 text on a 32,768-env line)."""
+    import json
+
+    b = _bench()
+    assert b.BASELINE_METRIC == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]

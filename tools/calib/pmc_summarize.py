@@ -1,8 +1,13 @@
-"""Calibrated hwy_step HBM bytes per launch from the pmc_step.sh passes -> profiles/hwy_step_pmc.json"""
+"""Calibrated hwy_step HBM bytes per launch from the pmc_step.sh passes
+    python3 tools/calib/pmc_summarize.py <dir> [E N F_out]
+-> profiles/hwy_step_pmc.json (E 4096, N 15, F_out 4) or profiles/hwy_step_pmc_E<E>_N<N>_F<F>.json"""
 import csv, glob, json, os, sys
 
 d = sys.argv[1]
-E, NF = 4096, 13
+E = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+N = int(sys.argv[3]) if len(sys.argv) > 3 else 15
+Fo = int(sys.argv[4]) if len(sys.argv) > 4 else 4
+NF = 13
 calib_bytes = NF * E * 64 * 4
 
 
@@ -24,7 +29,7 @@ kw = calib_bytes / write["calib_write"]
 step_read = fetch["hwy_step_kernel"] * kf
 step_write = write["hwy_step_kernel"] * kw
 res = {
-    "kernel": "hwy_step_kernel", "envs_per_launch": E,
+    "kernel": "hwy_step_kernel", "envs_per_launch": E, "obs_rows": N, "obs_features": Fo,
     "fetch_size_raw_bytes": fetch["hwy_step_kernel"], "write_size_raw_bytes": write["hwy_step_kernel"],
     "calib_read_raw_bytes": fetch["calib_read"], "calib_write_raw_bytes": write["calib_write"],
     "calib_true_bytes": calib_bytes, "fetch_scale": kf, "write_scale": kw,
@@ -35,4 +40,6 @@ res = {
 }
 print(json.dumps(res, indent=1))
 os.makedirs("profiles", exist_ok=True)
-json.dump(res, open("profiles/hwy_step_pmc.json", "w"), indent=1)
+out = ("profiles/hwy_step_pmc.json" if (E, N, Fo) == (4096, 15, 4)
+       else f"profiles/hwy_step_pmc_E{E}_N{N}_F{Fo}.json")
+json.dump(res, open(out, "w"), indent=1)

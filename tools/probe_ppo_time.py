@@ -1,6 +1,6 @@
 """Times the fused PPO update (graph of ppo_rows / ppo_wgrad / ppo_wsum / ppo_adam) at the bench
-minibatch (development aid): probe_ppo_time.py [H] [reps] [minibatch rows]; HWY_LIB overrides
-the library."""
+minibatch (development aid): probe_ppo_time.py [H] [reps] [minibatch rows] [S]; HWY_LIB
+overrides the library."""
 import os, sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "highway-rope-ppo_amd"))
@@ -13,7 +13,8 @@ from hwy.ppo_native import FusedPPO
 from ppo.agent import PPOAgent
 
 dev = torch.device("cuda", 0)
-S, H, nmb = 60, int(sys.argv[1]) if len(sys.argv) > 1 else 256, 32
+S = int(sys.argv[4]) if len(sys.argv) > 4 else 60
+H, nmb = int(sys.argv[1]) if len(sys.argv) > 1 else 256, 32
 mb = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 torch.manual_seed(0)

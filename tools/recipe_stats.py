@@ -13,14 +13,24 @@ REF = {42: 136.8270, 1042: 127.8022, 2042: 132.6172}  # artifacts/combined_valid
 
 
 def main(d, note=""):
+    global REF
     rows = [json.loads(l) for l in open(f"{d}/summary.jsonl")]
+    # the run's own reference cell when the summary carries it (PE conditions, hidden sweep)
+    own = {r["seed"]: r["reference_final_reward"] for r in rows if "reference_final_reward" in r}
+    if own:
+        REF = own
     fr = np.array([r["final_reward"] for r in rows])
-    out = {"note": note, "n": len(rows), "mean": round(float(fr.mean()), 2),
+    out = {"note": note, "condition": rows[0].get("condition"),
+           "hidden_dim": rows[0].get("hidden_dim", 256), "n": len(rows), "mean": round(float(fr.mean()), 2),
            "std": round(float(fr.std()), 2), "min": float(fr.min()), "max": float(fr.max()),
            "reference_mean_3seeds": round(float(np.mean(list(REF.values()))), 2), "per_seed": []}
     m3 = [r["final_reward"] for r in rows if r["seed"] in REF]
     if m3:
         out["matched_seeds_mean"] = round(float(np.mean(m3)), 2)
+        ref_mean = float(np.mean(list(REF.values())))
+        out["matched_delta"] = round(out["matched_seeds_mean"] - ref_mean, 2)
+        out["matched_in_band"] = bool(abs(out["matched_seeds_mean"] - ref_mean) <= 5.0)
+        out["mean_in_band"] = bool(abs(float(fr.mean()) - ref_mean) <= 5.0)
     band = np.mean(list(REF.values())) - 5.0
     for r in rows:
         ev = np.array(r["evals"])

@@ -39,6 +39,18 @@ REFERENCE_FINAL = {
     "shuffled_distpe": {42: 136.0069, 1042: 82.4615, 2042: 125.5533},
     "shuffled_rankpe": {42: 83.2977, 1042: 119.7457, 2042: 119.0862},
 }
+# the hidden-dim sweep of the sorted condition (the same CSV, rows sorted_..._hidden_dim{384,512}_
+# ..._batch_size64_d_embed4: d_embed is unused by the sorted condition)
+REFERENCE_FINAL_HIDDEN = {
+    ("sorted", 384): {42: 135.6114, 1042: 113.3057, 2042: 108.0399},
+    ("sorted", 512): {42: 118.0541, 1042: 110.4705, 2042: 127.7685},
+}
+
+
+def reference_final(condition: str, hidden: int) -> dict:
+    if hidden == 256:
+        return REFERENCE_FINAL[condition]
+    return REFERENCE_FINAL_HIDDEN.get((condition, hidden), {})
 
 
 def main():
@@ -54,6 +66,7 @@ def main():
     p.add_argument("--eval-interval", type=int, default=50)
     p.add_argument("--lr", type=float, default=3e-4)
     p.add_argument("--epochs", type=int, default=8)
+    p.add_argument("--hidden", type=int, default=256)
     args = p.parse_args()
 
     out = os.path.abspath(args.out)
@@ -70,12 +83,13 @@ def main():
             "shuffled_rankpe": Condition.SHUFFLED_RANKPE}[args.condition]
     d_embed = None if args.condition == "sorted" else 4
     for seed in args.seeds:
-        name = (f"{args.condition}_lr{args.lr:g}_hidden_dim256_clip_eps0.2_entropy_coef0.005_"
-                f"epochs{args.epochs}_batch_size64" + (f"_d_embed{d_embed}" if d_embed else "")
+        name = (f"{args.condition}_lr{args.lr:g}_hidden_dim{args.hidden}_clip_eps0.2_"
+                f"entropy_coef0.005_epochs{args.epochs}_batch_size64"
+                + (f"_d_embed{d_embed}" if d_embed else "")
                 + f"_seed{seed}" + (f"_envs{args.num_envs}" if args.num_envs > 1 else "")
                 + (f"_T{args.rollout}_mb{args.minibatches}" if args.rollout else ""))
         hp = ConditionHP(lr=args.lr, clip_eps=0.2, epochs=args.epochs, batch_size=64,
-                         hidden_dim=256, d_embed=d_embed)
+                         hidden_dim=args.hidden, d_embed=d_embed)
         hp.entropy_coef = 0.005
         if args.rollout:
             hp.steps_per_update = args.num_envs * args.rollout
@@ -99,7 +113,7 @@ def main():
         row = {"condition": args.condition, "seed": seed, "experiment": name, "status": res["status"], "wall_s": round(wall, 1),
                "num_envs": args.num_envs, "episodes": args.episodes, "rollout": args.rollout,
                "minibatches": args.minibatches, "eval_interval": args.eval_interval,
-               "lr": args.lr, "epochs": args.epochs,
+               "lr": args.lr, "epochs": args.epochs, "hidden_dim": args.hidden,
                "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else "cpu"}
         if res["status"] == "COMPLETED":
             avg = res["avg_rewards"]
@@ -110,7 +124,7 @@ def main():
                        eval_episodes=hist.get("eval_episode_numbers", []),
                        env_steps=int(sum(u.get("steps", 0) for u in ups)), updates=len(ups),
                        train_s=round(float(sum(u.get("time", 0.0) for u in ups)), 2))
-            ref = REFERENCE_FINAL[args.condition].get(seed)
+            ref = reference_final(args.condition, args.hidden).get(seed)
             if ref is not None:
                 row.update(reference_final_reward=ref,
                            delta=round(float(avg[-1]) - ref, 4))
@@ -126,8 +140,8 @@ def main():
     done = [r for r in results if "final_reward" in r]
     if done:
         mean = sum(r["final_reward"] for r in done) / len(done)
-        refs = [REFERENCE_FINAL[args.condition][r["seed"]] for r in done
-                if r["seed"] in REFERENCE_FINAL[args.condition]]
+        rf = reference_final(args.condition, args.hidden)
+        refs = [rf[r["seed"]] for r in done if r["seed"] in rf]
         print(json.dumps({"condition": args.condition, "mean_final_reward": round(mean, 4),
                           "reference_mean": round(sum(refs) / len(refs), 4) if refs else None,
                           "n": len(done)}), flush=True)
