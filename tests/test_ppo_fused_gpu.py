@@ -187,7 +187,10 @@ def _check_grads(ga, gb, g64, msg=""):
                                     # 26-32 tiles x 8 slices + extras; H 384: 60 tiles x 4
                                     # slices; H 512: 104 tiles x 2 slices)
                                     (120, 256, 32768), (120, 384, 32768), (120, 512, 32768),
-                                    (240, 256, 32768), (240, 384, 32768), (240, 512, 32768)])
+                                    (240, 256, 32768), (240, 384, 32768), (240, 512, 32768),
+                                    # ppo_rowsT (64-row workgroups, >= 64 rows per CU) at the
+                                    # narrower learners: 4, 8 and 12 output blocks per layer
+                                    (60, 64, 16384), (60, 128, 16384), (136, 192, 16384)])
 def test_fused_gradient_matches_autograd(S, H, mb):
     """One fused forward/backward against autograd on the same minibatch.  The reference
     gradient is float64 autograd: at S = 240 / H = 512 and 4096 rows torch's own fp32 GEMMs
