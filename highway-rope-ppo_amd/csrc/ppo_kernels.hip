@@ -493,13 +493,14 @@ inline bool fused_ok(const hwy_ppo_dims& d) {
 
 inline int head_stride(int H) { return 3 * H + 16; }
 
-// ppo_rowsT (the transposed row kernel, 64 rows per workgroup) when the minibatch gives every CU
-// a workgroup: H <= 256 and B a multiple of 64 with B >= 64 x CUs (16,384 rows on MI355X)
+// ppo_rowsT (the transposed row kernel, 64 rows per workgroup) where the minibatch gives every
+// CU a workgroup (H <= 256, B a multiple of 64, B >= 64 x CUs).  Measured slower than ppo_rows
+// (146 against 125 us at 16,384 rows), so only a development build selects it (HWY_ROWS_T=1).
 constexpr int kTRowsWG = 64;
 inline bool rows_t_ok(const hwy_ppo_dims& d) {
   return fused_ok(d) && d.H <= 256 && d.B % kTRowsWG == 0 &&
          (int64_t)d.B >= (int64_t)kTRowsWG * chip_geom().cus &&
-         dev_knob_int("HWY_ROWS_T", 1) != 0;
+         dev_knob_int("HWY_ROWS_T", 0) != 0;
 }
 constexpr int kRedThreads = 256;
 
