@@ -73,6 +73,12 @@ constexpr int kMaxRowS = 256;  // states dim bound of the fused path (LDS)
 #ifndef HWY_ROWS_NW
 #define HWY_ROWS_NW 8  // ppo_rows waves at H = 256 (16: 4 per SIMD, one 16-column tile each)
 #endif
+#ifndef HWY_ROWS_CMP
+#define HWY_ROWS_CMP 1  // ppo_rows' compact LDS at H = 256, 32-row tiles (two workgroups per CU)
+#endif
+#ifndef HWY_RING_DC
+#define HWY_RING_DC 2  // weight blocks in flight per wave in the compact-LDS ppo_rows
+#endif
 #ifndef HWY_ROWS_NW32
 #define HWY_ROWS_NW32 8  // the same for the 32-row tiles
 #endif
@@ -807,10 +813,13 @@ struct WRing {
   __device__ __forceinline__ void load_blk(const float* W, int ldw, int nn, int kb,
                                            f32x4 (&dst)[TW]) {
     if constexpr (TL) {  // tile image (TileGeom): one contiguous KB per 16 columns and block
-      const float* p = W + ((long)(n_base / 16) * ldw + (kb >> 4)) * 256 + (16 * g + c) * 4;
+      // wave-uniform tile address (scalar registers) + the lane's float4 (16 g + c = lane)
+      const int tile0 = __builtin_amdgcn_readfirstlane((n_base / 16) * ldw + (kb >> 4));
+      const float* p = W + (long)tile0 * 256;
+      const int lo = 4 * (16 * g + c);
 #pragma unroll
       for (int t = 0; t < TW; ++t)
-        dst[t] = *reinterpret_cast<const f32x4*>(p + (long)t * ldw * 256);
+        dst[t] = *reinterpret_cast<const f32x4*>(p + (long)t * ldw * 256 + lo);
       return;
     }
     const int k = kb + 4 * g;
@@ -833,7 +842,9 @@ struct WRing {
     const int ldw = nxt ? s1.ldw : s0.ldw, nn = nxt ? s1.nn : s0.nn, K = nxt ? s1.K : s0.K;
     int kb = nxt ? 16 * (b - s0.nblk) : 16 * b;
     if (SEG + 1 >= NSEG && nxt) kb = 0;
-    kb = min(kb, K - 4 - 4 * g);  // k + 3 < K for every lane (K % 4 == 0)
+    // k + 3 < K for every lane (K % 4 == 0); a tile image holds whole (zero-padded) blocks, so
+    // its block index stays wave-uniform
+    if constexpr (!TL) kb = min(kb, K - 4 - 4 * g);
     load_blk(W, ldw, nn, kb, dst);
   }
   __device__ __forceinline__ void prime() {
@@ -904,8 +915,10 @@ __device__ __forceinline__ void ring_setup(WRing<TW, D, NSEG, TL>& R, const floa
   R.g = lane >> 4;
   R.c = lane & 15;
   R.n_base = n_base;
-  const int hb = (H / 16 + D - 1) / D * D;
-  const int sb = ((S + 15) / 16 + D - 1) / D * D;
+  // the blocks of the tile image (rows_blocks: multiples of the default ring depth, which every
+  // ring depth used here divides)
+  int sb, hb;
+  rows_blocks(S, H, &sb, &hb);
   if constexpr (TL) {
     const TileGeom T = tile_geom(S, H, sb, hb);
     const WSeg all[7] = {{tiles + T.f1, sb, 16 * sb, sb, 2},  {tiles + T.f2, hb, H, hb, 2},
@@ -942,6 +955,52 @@ __device__ __forceinline__ void row_epi_bias_relu(const f32x4 (&acc)[RB][TW],
         float v = acc[rb][t][r] + bn;
         v = v > 0.0f ? v : 0.0f;
         out[row * po + n] = v;
+      }
+    }
+}
+
+// row_epi_bias_relu that also returns the ReLU decisions of the lane's C elements as bits
+// (bit (rb TW + t) 4 + r: the output is > 0), for the backward's masks
+template <int RB, int TW>
+__device__ __forceinline__ uint32_t row_epi_bias_relu_bits(const f32x4 (&acc)[RB][TW],
+                                                           const float (&bias)[TW], float* out,
+                                                           int po, int n_base) {
+  static_assert(RB * TW * 4 <= 32, "mask bits: one 32-bit word per lane");
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  uint32_t m = 0u;
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      const int n = n_base + 16 * t + c;
+      const float bn = bias[t];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * rb + 4 * g + r;
+        float v = acc[rb][t][r] + bn;
+        v = v > 0.0f ? v : 0.0f;
+        out[row * po + n] = v;
+        m |= (v > 0.0f ? 1u : 0u) << ((rb * TW + t) * 4 + r);
+      }
+    }
+  return m;
+}
+
+// the layer's output gradient through the ReLU decisions kept as bits (row_epi_bias_relu_bits)
+// into the LDS image `out`: the same value row_epi_mask writes
+template <int RB, int TW>
+__device__ __forceinline__ void row_epi_maskbits(const f32x4 (&acc)[RB][TW], uint32_t m, float* out,
+                                                 int po, int n_base) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      const int n = n_base + 16 * t + c;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * rb + 4 * g + r;
+        out[row * po + n] = ((m >> ((rb * TW + t) * 4 + r)) & 1u) ? acc[rb][t][r] : 0.0f;
       }
     }
 }
@@ -1009,12 +1068,14 @@ __device__ __forceinline__ void rows_out(const float* img, int pitch, float* g, 
 // X may alias AC (it is dead once h1 is computed).  Ends with a workgroup barrier.
 // KEEP: [a1 | c1] stays in the layer-3 accumulators (a1 -> av, c1 -> cv, after bias and ReLU)
 // instead of going to AC, and the function ends without the barrier.
-template <int QH, int NW, int RT, bool KEEP, int D, int NSEG, bool TL>
+// MSK: the ReLU decisions of h1 and h2 (this lane's C elements) also go to mb[0], mb[1] as bits
+// (row_epi_bias_relu_bits), so the backward needs neither image for its masks.
+template <int QH, int NW, int RT, bool KEEP, int D, int NSEG, bool TL, bool MSK = false>
 __device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG, TL>& R, const float* states,
                                              const int64_t* idx, int S, int nrows, int row0,
                                              const float* P, const int64_t* off, float* X,
                                              float* H1, float* H2, float* AC, float* xg,
-                                             float* h1g, float* h2g,
+                                             float* h1g, float* h2g, uint32_t (&mb)[2],
                                              f32x4 (&av)[RT / 16][H_TW(QH, NW)],
                                              f32x4 (&cv)[RT / 16][H_TW(QH, NW)] PSEC_PARAMS) {
   constexpr int H = 64 * QH;
@@ -1033,8 +1094,10 @@ __device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG, TL>& R
 #pragma unroll
       for (int u = 0; u < TW; ++u) bias[l][u] = P[bo[l] + R.n_base + 16 * u + c];
   }
-  // zero-padded to whole ring groups of 16-deep blocks
-  const int Sp = ((S + 15) / 16 + D - 1) / D * D * 16, px = row_pitch(Sp);
+  // zero-padded to whole ring groups of 16-deep blocks (the ring's layer-1 segment, rows_blocks)
+  int sbk, hbk;
+  rows_blocks(S, H, &sbk, &hbk);
+  const int Sp = 16 * sbk, px = row_pitch(Sp);
   // states rows, zero-padded to Sp columns and RT rows
   for (int e = t; e < RT * (Sp / 4); e += NT) {
     const int row = e / (Sp / 4), k = 4 * (e % (Sp / 4));
@@ -1053,14 +1116,20 @@ __device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG, TL>& R
   // h1 = relu(x W1^T + b1)
   zero_acc(acc);
   R.template run<0>(X, px, acc);
-  row_epi_bias_relu(acc, bias[0], H1, PH, nb);
+  if constexpr (MSK)
+    mb[0] = row_epi_bias_relu_bits(acc, bias[0], H1, PH, nb);
+  else
+    row_epi_bias_relu(acc, bias[0], H1, PH, nb);
   __syncthreads();
   if (h1g) rows_out<NT, RT>(H1, PH, h1g + (long)row0 * H, H, H, nrows);
   PSEC(1);
   // h2 = relu(h1 W2^T + b2)
   zero_acc(acc);
   R.template run<1>(H1, PH, acc);
-  row_epi_bias_relu(acc, bias[1], H2, PH, nb);
+  if constexpr (MSK)  // H2 may alias X: every wave is past layer 1's reads (the barrier above)
+    mb[1] = row_epi_bias_relu_bits(acc, bias[1], H2, PH, nb);
+  else
+    row_epi_bias_relu(acc, bias[1], H2, PH, nb);
   __syncthreads();
   if (h2g) rows_out<NT, RT>(H2, PH, h2g + (long)row0 * H, H, H, nrows);
   PSEC(2);
@@ -1083,8 +1152,14 @@ __device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG, TL>& R
   __syncthreads();
 }
 
-template <int QH, int NW, int RT>
-__global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
+// CMP (compact LDS, H 256 at 32-row tiles): one region of two H-wide row images P0 | P1 holds,
+// in turn, the states (P1), h1 (P0), h2 (P1), dac (across both, pitch PA), dh2 (P0) and dh1 (P1);
+// the ReLU decisions of h1 / h2 stay in registers as bits.  72.6 KB instead of 139 KB, so two
+// workgroups share a CU (4 waves per SIMD, <= 128 VGPRs) and one's phase boundaries, gather and
+// loss head overlap the other's MFMAs.  One extra barrier: dh2 overwrites dac's image only after
+// every wave has finished reading it.
+template <int QH, int NW, int RT, bool CMP>
+__device__ __forceinline__ void rows_body(const RowArgs& r) {
   constexpr int H = 64 * QH;
   constexpr int TW = H / NW / 16;        // 16-column output tiles per wave
   constexpr int RB = RT / 16;            // 16-row blocks per workgroup
@@ -1094,24 +1169,27 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   static_assert(RT % 16 == 0 && RPW >= 1 && RPW <= 16, "RT: whole 16-row blocks, <= 16 head rows per wave");
   constexpr int PH = lds_pitch(H), PA = lds_pitch(2 * H), PXMAX = lds_pitch(kMaxRowS);
   // the states image lives in [a1|c1] when its rows fit (it is dead before dac is written there)
-  constexpr bool kOwnX = PXMAX > PA;
+  constexpr bool kOwnX = !CMP && PXMAX > PA;
+  static_assert(!CMP || (PA <= 2 * PH && PXMAX <= PH), "CMP: dac spans P0 | P1, the states fit P1");
   __shared__ __attribute__((aligned(16))) float XX[kOwnX ? RT * PXMAX : 4];
-  __shared__ __attribute__((aligned(16))) float H1[RT * PH];
-  __shared__ __attribute__((aligned(16))) float H2[RT * PH];
-  __shared__ __attribute__((aligned(16))) float AC[RT * PA];
+  __shared__ __attribute__((aligned(16))) float H1[CMP ? 2 * RT * PH : RT * PH];  // CMP: P0 | P1
+  __shared__ __attribute__((aligned(16))) float H2[CMP ? 4 : RT * PH];
+  __shared__ __attribute__((aligned(16))) float ACI[CMP ? 4 : RT * PA];
+  float* const P1 = CMP ? H1 + RT * PH : H2;  // h2 (and, CMP, the states, then dh1)
+  float* const AC = CMP ? H1 : ACI;            // [a1 | c1] / dac image
   // the loss head works from the layer-3 accumulators: per-wave partial dot products of every
   // row, the per-row output scalars, the per-wave metric / bias / log_std sums
   __shared__ __attribute__((aligned(16))) f32x4 HDOT[NW][RT];
   __shared__ __attribute__((aligned(16))) f32x4 HROW[RT];
   __shared__ float HTAIL[NW][12];
-  float* X = kOwnX ? XX : AC;
+  float* X = CMP ? P1 : (kOwnX ? XX : AC);
   PSEC_DECL
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int S = r.S;
   const int row0 = blockIdx.x * RT;
   const int nrows = min(RT, r.B - row0);
   const float* P = r.params;
-  constexpr int D = ring_depth<TW>();
+  constexpr int D = CMP ? HWY_RING_DC : ring_depth<TW>();  // CMP: 4 waves per SIMD hide more
   WRing<TW, D, 7, true> R;
   ring_setup(R, P, r.off, S, H, w * (H / NW), r.tiles);
   R.prime();
@@ -1130,6 +1208,10 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
     hadv = r.adv[src];
     hret = r.ret[src];
   }
+  // the squash correction depends on the stored pre-tanh actions only: computed here, its
+  // latency hides behind the forward instead of lengthening the loss head's dependent chain
+  const float hq0 = log1pf(-(tanhf(hz0) * tanhf(hz0)) + 1e-6f);
+  const float hq1 = log1pf(-(tanhf(hz1) * tanhf(hz1)) + 1e-6f);
   float wa0[TW], wa1[TW], wc[TW];
 #pragma unroll
   for (int u = 0; u < TW; ++u) {
@@ -1141,8 +1223,10 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   const float ba0 = P[r.off[P_BA2]], ba1 = P[r.off[P_BA2] + 1], bcv = P[r.off[P_BC2]];
   const float ls0 = P[r.off[P_LOGSTD]], ls1 = P[r.off[P_LOGSTD] + 1];
   f32x4 av[RB][TW], cv[RB][TW];  // a1, c1 of this wave's columns (C layout)
-  rows_forward<QH, NW, RT, true>(R, r.states, r.idx, S, nrows, row0, P, r.off, X, H1, H2, AC,
-                                 r.xg, r.h1, r.h2, av, cv PSEC_ARGS);
+  uint32_t mb[2] = {0u, 0u};      // CMP: ReLU decisions of h1, h2 (this lane's C elements)
+  rows_forward<QH, NW, RT, true, D, 7, true, CMP>(R, r.states, r.idx, S, nrows, row0, P, r.off, X,
+                                                  H1, P1, AC, r.xg, r.h1, r.h2, mb, av,
+                                                  cv PSEC_ARGS);
   PSEC(3);
   const int g4 = lane >> 4, c16 = lane & 15;
 
@@ -1181,10 +1265,9 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
     for (int ww = 1; ww < NW; ++ww) dsum += HDOT[ww][hr];
     const float mu0 = dsum[0] + ba0, mu1 = dsum[1] + ba1, val = dsum[2] + bcv;
     const float d0 = hz0 - mu0, d1 = hz1 - mu1;
-    const float t0 = tanhf(hz0), t1 = tanhf(hz1);
     const float lp0 = -(d0 * d0) / (2.0f * var0) - lsc0 - LOG_SQRT_2PI;
     const float lp1 = -(d1 * d1) / (2.0f * var1) - lsc1 - LOG_SQRT_2PI;
-    const float logp = (lp0 - log1pf(-(t0 * t0) + 1e-6f)) + (lp1 - log1pf(-(t1 * t1) + 1e-6f));
+    const float logp = (lp0 - hq0) + (lp1 - hq1);
     const float log_ratio = logp - hold;
     const float ratio = expf(log_ratio);
     const float cr = fminf(fmaxf(ratio, lo), hi);
@@ -1278,18 +1361,40 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
   zero_acc(acc);
   R.template run<4>(AC, PA, acc);
   R.template run<5>(AC + H, PA, acc);
-  row_epi_mask(acc, H2, PH, nb);
+  float* const DH2 = CMP ? H1 : H2;  // CMP: P0
+  float* const DH1 = CMP ? P1 : H1;
+  if constexpr (CMP) {
+    __syncthreads();  // every wave has read dac (P0 | P1)
+    row_epi_maskbits(acc, mb[1], DH2, PH, nb);
+  } else {
+    row_epi_mask(acc, H2, PH, nb);
+  }
   __syncthreads();
-  if (r.dh2) rows_out<NT, RT>(H2, PH, r.dh2 + (long)row0 * H, H, H, nrows);
+  if (r.dh2) rows_out<NT, RT>(DH2, PH, r.dh2 + (long)row0 * H, H, H, nrows);
   PSEC(5);
   // dh1 = (dh2 W2) * (h1 > 0)
   zero_acc(acc);
-  R.template run<6>(H2, PH, acc);
-  row_epi_mask(acc, H1, PH, nb);  // dh1 over h1 (same thread)
+  R.template run<6>(DH2, PH, acc);
+  if constexpr (CMP)
+    row_epi_maskbits(acc, mb[0], DH1, PH, nb);  // P1: dac is dead, dh2 is in P0
+  else
+    row_epi_mask(acc, H1, PH, nb);  // dh1 over h1 (same thread)
   __syncthreads();
-  if (r.dh1) rows_out<NT, RT>(H1, PH, r.dh1 + (long)row0 * H, H, H, nrows);
+  if (r.dh1) rows_out<NT, RT>(DH1, PH, r.dh1 + (long)row0 * H, H, H, nrows);
   PSEC(6);
   PSEC_FLUSH;
+}
+
+template <int QH, int NW, int RT>
+__global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
+  rows_body<QH, NW, RT, false>(r);
+}
+
+// the compact-LDS variant: two workgroups per CU, so at most 128 VGPRs (4 waves per SIMD)
+template <int QH, int NW, int RT>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2 * NW / 4, 8)))
+ppo_rows_c(RowArgs r) {
+  rows_body<QH, NW, RT, true>(r);
 }
 
 // ----------------------------------------------------------------------------- ppo_rowsT
@@ -1515,6 +1620,8 @@ __global__ void __launch_bounds__(256, 1) ppo_rowsT(RowArgs r) {
   }
   const long src_row = (long)r.idx[myrow];
   const float hz0 = r.pre_tanh[src_row * 2], hz1 = r.pre_tanh[src_row * 2 + 1];
+  const float hq0 = log1pf(-(tanhf(hz0) * tanhf(hz0)) + 1e-6f);
+  const float hq1 = log1pf(-(tanhf(hz1) * tanhf(hz1)) + 1e-6f);
   const float hold = r.old_logp[src_row], hadv = r.adv[src_row], hret = r.ret[src_row];
   const float ba0 = P[r.off[P_BA2]], ba1 = P[r.off[P_BA2] + 1], bcv = P[r.off[P_BC2]];
   const float ls0 = P[r.off[P_LOGSTD]], ls1 = P[r.off[P_LOGSTD] + 1];
@@ -1636,10 +1743,9 @@ __global__ void __launch_bounds__(256, 1) ppo_rowsT(RowArgs r) {
     const float lo = 1.0f - r.eps_clip, hi = 1.0f + r.eps_clip;
     const float mu0 = p0 + ba0, mu1 = p1 + ba1, val = pv + bcv;
     const float d0 = hz0 - mu0, d1 = hz1 - mu1;
-    const float t0 = tanhf(hz0), t1 = tanhf(hz1);
     const float lp0 = -(d0 * d0) / (2.0f * var0) - lsc0 - LOG_SQRT_2PI;
     const float lp1 = -(d1 * d1) / (2.0f * var1) - lsc1 - LOG_SQRT_2PI;
-    const float logp = (lp0 - log1pf(-(t0 * t0) + 1e-6f)) + (lp1 - log1pf(-(t1 * t1) + 1e-6f));
+    const float logp = (lp0 - hq0) + (lp1 - hq1);
     const float log_ratio = logp - hold;
     const float ratio = expf(log_ratio);
     const float cr = fminf(fmaxf(ratio, lo), hi);
@@ -1802,8 +1908,9 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_act(ActArgs r) {
   uint64_t _pt = 0, _pacc[16];
 #endif
   f32x4 unused_a[kRowTile / 16][TW], unused_c[kRowTile / 16][TW];
+  uint32_t unused_m[2];
   rows_forward<QH, NW, kRowTile, false>(R, r.states, nullptr, r.S, nrows, row0, P, r.off, X, H1,
-                                        H2, AC, nullptr, nullptr, nullptr, unused_a,
+                                        H2, AC, nullptr, nullptr, nullptr, unused_m, unused_a,
                                         unused_c PSEC_ARGS);
   float wa0[QH], wa1[QH], wc[QH];
 #pragma unroll
@@ -2017,22 +2124,24 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int tile_id, int kb0
   // features past M / N hold finite in-range data whose outputs are never stored.
   const int ca = lane & 31, ra = lane >> 5, cb = lane & 15, rb = lane >> 4;
   const bool stage_b = w < 4;
-  const float* a_src = A + min(i0 + 4 * ca, M - 4);
-  const float* b_src = Bm + min(j0 + 4 * cb, N - 4);
+  // element offsets from the (wave-uniform) matrix bases fit 32 bits (B <= 2^20 rows of <= 512
+  // floats): scalar base + one 32-bit VGPR offset per load instead of a 64-bit lane address
+  const uint32_t a_col = (uint32_t)min(i0 + 4 * ca, M - 4);
+  const uint32_t b_col = (uint32_t)min(j0 + 4 * cb, N - 4);
   // two register sets: the loads of chunk c + 2 are in flight while chunk c computes and chunk
   // c + 1 (loaded during chunk c - 1) is staged
   f32x4 pa0[4], pb0[4], pa1[4], pb1[4];
   auto fetch = [&](int k0, f32x4(&pa)[4], f32x4(&pb)[4]) {
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
-      const int k = min(k0 + 8 * w + 4 * ra + jj, kb1 - 1);
-      pa[jj] = *reinterpret_cast<const f32x4*>(a_src + (long)k * lda);
+      const uint32_t k = (uint32_t)min(k0 + 8 * w + 4 * ra + jj, kb1 - 1);
+      pa[jj] = *reinterpret_cast<const f32x4*>(A + (k * (uint32_t)lda + a_col));
     }
     if (stage_b) {
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
-        const int k = min(k0 + 16 * w + 4 * rb + jj, kb1 - 1);
-        pb[jj] = *reinterpret_cast<const f32x4*>(b_src + (long)k * ldb);
+        const uint32_t k = (uint32_t)min(k0 + 16 * w + 4 * rb + jj, kb1 - 1);
+        pb[jj] = *reinterpret_cast<const f32x4*>(Bm + (k * (uint32_t)ldb + b_col));
       }
     }
   };
@@ -2613,7 +2722,12 @@ int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
         case 1: hipLaunchKernelGGL((ppo_rows<1, 4, 32>), g1, b4, 0, s, r); break;
         case 2: hipLaunchKernelGGL((ppo_rows<2, 8, 32>), g1, b8, 0, s, r); break;
         case 3: hipLaunchKernelGGL((ppo_rows<3, 4, 32>), g1, b4, 0, s, r); break;
-        default: hipLaunchKernelGGL((ppo_rows<4, HWY_ROWS_NW32, 32>), g1, dim3(64 * HWY_ROWS_NW32), 0, s, r); break;
+        default:
+          if (HWY_ROWS_CMP && HWY_ROWS_NW32 == 8)
+            hipLaunchKernelGGL((ppo_rows_c<4, 8, 32>), g1, b8, 0, s, r);
+          else
+            hipLaunchKernelGGL((ppo_rows<4, HWY_ROWS_NW32, 32>), g1, dim3(64 * HWY_ROWS_NW32), 0, s, r);
+          break;
       }
     } else {
       switch (H / 64) {
