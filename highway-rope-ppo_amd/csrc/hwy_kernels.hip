@@ -550,6 +550,7 @@ __device__ void observe_wave(const hwy_config& C, int lane, const Veh& v, float 
 }
 
 // ------------------------------------------------------------------------- state I/O
+
 __device__ __forceinline__ void load_veh(const uint32_t* st, size_t fstride, uint32_t idx, int lane,
                                          int V, Veh& v, int& order_pos) {
   v.x = hm_bits2f((st + HWY_F_X * fstride)[idx]);
@@ -574,9 +575,12 @@ __device__ __forceinline__ void load_veh(const uint32_t* st, size_t fstride, uin
 
 __device__ __forceinline__ void store_veh(uint32_t* st, size_t fstride, uint32_t idx, int lane, int V,
                                           const Veh& v, int order_pos) {
-  // opaque copy of the offset: the 13 field addresses are rebuilt here instead of being kept
-  // live (26 VGPRs) from load_veh across the whole step
+  // opaque copies of the offset, the base and the field stride: the 13 field addresses are
+  // rebuilt here instead of being kept live from load_veh across the whole step (26 VGPRs for the
+  // lane addresses, 26 SGPRs for the field bases, which otherwise spill the frame loop's scalars)
   asm volatile("" : "+v"(idx));
+  asm volatile("" : "+s"(st));
+  asm volatile("" : "+s"(fstride));
   const bool live = lane < V;
   (st + HWY_F_X * fstride)[idx] = live ? hm_f2bits(v.x) : 0u;
   (st + HWY_F_Y * fstride)[idx] = live ? hm_f2bits(v.y) : 0u;
@@ -600,6 +604,8 @@ __device__ __forceinline__ void store_env_words(uint32_t* st, size_t fstride, ui
                                                 int step, int episode, uint64_t seed, float ego_acc,
                                                 float ego_steer, float ep_return) {
   asm volatile("" : "+v"(idx));
+  asm volatile("" : "+s"(st));
+  asm volatile("" : "+s"(fstride));
   uint32_t w = 0u;
   if (lane == HWY_E_STEP) w = (uint32_t)step;
   if (lane == HWY_E_EPISODE) w = (uint32_t)episode;

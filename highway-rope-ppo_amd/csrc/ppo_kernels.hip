@@ -76,6 +76,14 @@ constexpr int kMaxRowS = 256;  // states dim bound of the fused path (LDS)
 #ifndef HWY_ROWS_CMP
 #define HWY_ROWS_CMP 1  // ppo_rows' compact LDS at H = 256, 32-row tiles (two workgroups per CU)
 #endif
+#ifndef HWY_WG_EXP
+// timing-only ppo_wgrad experiments (wrong results; development builds): 1 no LDS staging, 2 no
+// global loads after the first chunk, 3 no barriers in the chunk loop, 4 no MFMAs
+#define HWY_WG_EXP 0
+#endif
+#ifndef HWY_WG_DMA
+#define HWY_WG_DMA 1  // ppo_wgrad stages its chunks by LDS-DMA (wgrad_tile_dma); 0: register staging
+#endif
 #ifndef HWY_RING_DC
 #define HWY_RING_DC 2  // weight blocks in flight per wave in the compact-LDS ppo_rows
 #endif
@@ -2091,9 +2099,187 @@ __device__ void wgrad_head(const WgArgs& a, int hid, float* lds, float* red) {
 
 #define WG_ST(p, v) (*(p) = (v))  // (nontemporal partial stores measured slower in ppo_wsum)
 
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// ppo_wgrad's chunk loop with LDS-DMA staging (HWY_WG_DMA, the default).  Chunks of 64 rows go
+// global -> LDS by global_load_lds_dwordx4 (1 KB per wave instruction, no VGPRs, no VALU) into
+// row-major images: A = 64 rows x 128 features (32 pieces of 2 rows), B = 64 rows x 64 features
+// (16 pieces of 4 rows); each wave issues 4 A and 2 B pieces per chunk.  Odd rows are stored
+// rotated by 32 floats (the rotation goes on the per-lane SOURCE address: the DMA destination is
+// lane-linear), so the MFMA operand reads -- one ds_read_b32 per operand and k-step, lanes 0-31
+// row 2s, lanes 32-63 row 2s + 1 of the same 32 features -- hit 64 distinct banks.  Three
+// buffers: chunk c + 2 is issued right after the barrier that opens chunk c (every wave has
+// finished reading chunk c - 1, whose buffer it reuses), and stays in flight across the next
+// barrier (counted vmcnt, raw s_barrier).  The register-staged loop spent 14 us of a 75 us
+// launch in its transposing staging (timing-only build without it: 61 us).
+// The A column sums (bias gradients) come from the A operand values in registers.
+[[maybe_unused]] __device__ __forceinline__ void wgrad_tile_dma(const WgArgs& a, int tile_id, int kb0, int kb1,
+                                               float* part, float* wg_lds PSEC_PARAMS) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, l32 = lane & 31;
+  const int H = a.H;
+  if (kb1 <= kb0) {
+    for (int i = t; i < kWgPart; i += 64 * kWgWaves) part[i] = 0.0f;
+    return;
+  }
+  int id = tile_id;
+  const float *A, *Bm;
+  int lda, ldb, M, N, ntj;
+  if (id < a.tac) {  // dWac = dac^T h2
+    A = a.dac, lda = 2 * H, Bm = a.h2, ldb = H, M = 2 * H, N = H;
+  } else if (id < a.tac + a.t2) {  // dW2 = dh2^T h1
+    id -= a.tac;
+    A = a.dh2, lda = H, Bm = a.h1, ldb = H, M = H, N = H;
+  } else {  // dW1 = dh1^T x (gathered states rows written by ppo_rows)
+    id -= a.tac + a.t2;
+    A = a.dh1, lda = H, Bm = a.xg, ldb = a.S, M = H, N = a.S;
+  }
+  ntj = (N + kWgTN - 1) / kWgTN;
+  const int ti = id / ntj, tj = id % ntj;
+  const int i0 = ti * kWgTM, j0 = tj * kWgTN;
+  const int nchunk = (kb1 - kb0 + 63) / 64;  // >= 1
+  constexpr int BUF = (kWgTM + kWgTN) * 64;  // floats per chunk buffer (48 KB)
+
+  // DMA sources (element offsets from the wave-uniform bases; 32 bits suffice).  A piece 4w + i:
+  // rows 2(4w + i) + h, lanes l32 -> feature quad l32 (even row) / (l32 - 8) & 31 (odd row);
+  // B piece 2w + i: rows 4(2w + i) + (lane >> 4), quad lane & 15 / (lane - 8) & 15 (odd row).
+  // Rows past the range load the last row (zeroed in the operands below); features past M / N
+  // load in-range duplicates whose outputs are never stored.
+  const int rb = lane >> 4, qb = lane & 15;
+  const uint32_t a_col = (uint32_t)min(i0 + 4 * (h ? ((l32 - 8) & 31) : l32), M - 4);
+  const uint32_t b_col = (uint32_t)min(j0 + 4 * ((rb & 1) ? ((qb - 8) & 15) : qb), N - 4);
+  auto dma = [&](int c, float* buf) {
+    const int k0 = kb0 + 64 * c;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t row = (uint32_t)min(k0 + 2 * (4 * w + i) + h, kb1 - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(A + (row * (uint32_t)lda + a_col)),
+                                       (lds_void_t*)(buf + (4 * w + i) * 256), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint32_t row = (uint32_t)min(k0 + 4 * (2 * w + i) + rb, kb1 - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(Bm + (row * (uint32_t)ldb + b_col)),
+                                       (lds_void_t*)(buf + kWgTM * 64 + (2 * w + i) * 256), 16,
+                                       0, 0);
+    }
+  };
+  // MFMA: waves w and w + 4 (one SIMD) own the same 64 x 32 output block (two 32x32
+  // accumulators sharing the B operand), over rows 0-31 / 32-63 of every chunk.
+  const int kh = w >> 2, wq = w & 3;
+  const int wm = (wq & 1) * 64, wn = (wq >> 1) * 32;
+  // per-lane operand offsets within a chunk image (row 2s + h, rotated odd rows)
+  const int offa0 = h * 128 + ((wm + l32 + 32 * h) & 127);
+  const int offa1 = h * 128 + ((wm + 32 + l32 + 32 * h) & 127);
+  const int offb = kWgTM * 64 + h * 64 + ((wn + l32 + 32 * h) & 63);
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc0[q] = acc1[q] = 0.0f;
+  float bs0 = 0.0f, bs1 = 0.0f;  // A column sums of this lane's features over its rows
+  auto compute = [&](const float* buf, int lim, auto mask_tag) {
+    constexpr bool MASK = decltype(mask_tag)::value;  // rows >= lim (of the chunk) are zero
+    const float* pa0 = buf + offa0 + 32 * kh * 128;
+    const float* pa1 = buf + offa1 + 32 * kh * 128;
+    const float* pb = buf + offb + 32 * kh * 64;
+    float x0[2][4], x1[2][4], y[2][4];
+    auto rd = [&](int g, int b) {  // k-steps 4g .. 4g + 3 of this wave's 16
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int st = 4 * g + j;
+        x0[b][j] = pa0[st * 256];
+        x1[b][j] = pa1[st * 256];
+        y[b][j] = pb[st * 128];
+      }
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int b = g & 1;
+      // the next group's reads go out before this group's MFMAs (pinned: the scheduler would
+      // otherwise sink them to their use and wait for them there)
+      if (g + 1 < 4) rd(g + 1, b ^ 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float u0 = x0[b][j], u1 = x1[b][j];
+        if constexpr (MASK) {
+          const bool live = 32 * kh + 2 * (4 * g + j) + h < lim;
+          u0 = live ? u0 : 0.0f;
+          u1 = live ? u1 : 0.0f;
+        }
+        bs0 += u0;
+        bs1 += u1;
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(u0, y[b][j], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(u1, y[b][j], acc1, 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  const std::integral_constant<bool, true> masked;
+  const std::integral_constant<bool, false> unmasked;
+  float* b0 = wg_lds;
+  float* b1 = wg_lds + BUF;
+  float* b2 = wg_lds + 2 * BUF;
+  // earlier stores of this wave (a previous tile's partial) drained: the vmcnt counts are exact
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  dma(0, b0);
+  if (nchunk > 1) dma(1, b1);
+  auto step = [&](int c, auto mask_tag) {
+    // this wave's pieces of chunk c landed (chunk c + 1's 6 may still be in flight) and its
+    // reads of chunk c - 1 returned; after the barrier, every wave's
+    if (c + 1 < nchunk)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (c + 2 < nchunk) dma(c + 2, b2);  // into chunk c - 1's buffer
+    compute(b0, kb1 - (kb0 + 64 * c), mask_tag);
+    float* tb = b0;
+    b0 = b1, b1 = b2, b2 = tb;
+  };
+  // whole chunks, then (ragged minibatches only) the last, partial one with its rows masked
+  const int nfull = (kb1 - kb0) / 64;
+  for (int c = 0; c < nfull; ++c) step(c, unmasked);
+  if (nfull < nchunk) step(nfull, masked);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  PSEC(8);
+  // bias sums over the wave's two row halves (lanes l, l + 32), then the two waves of a SIMD
+  bs0 += __shfl_xor(bs0, 32);
+  bs1 += __shfl_xor(bs1, 32);
+  // waves 4-7 hand their accumulators (and bias sums) to waves 0-3 through LDS
+  float* xch = wg_lds;                    // [4 waves][32 floats][64 lanes]
+  float* bx = wg_lds + 4 * 32 * 64;       // [4 waves][2][32]
+  if (kh == 1) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      xch[(wq * 32 + q) * 64 + lane] = acc0[q];
+      xch[(wq * 32 + 16 + q) * 64 + lane] = acc1[q];
+    }
+    if (h == 0) {
+      bx[(wq * 2) * 32 + l32] = bs0;
+      bx[(wq * 2 + 1) * 32 + l32] = bs1;
+    }
+  }
+  __syncthreads();
+  if (kh == 0) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int ri = wm + (q & 3) + 8 * (q >> 2) + 4 * h;
+      WG_ST(&part[ri * kWgTN + wn + l32], acc0[q] + xch[(wq * 32 + q) * 64 + lane]);
+      WG_ST(&part[(ri + 32) * kWgTN + wn + l32], acc1[q] + xch[(wq * 32 + 16 + q) * 64 + lane]);
+    }
+    if (tj == 0 && wn == 0 && h == 0) {  // waves 0, 1: features wm .. wm + 63
+      WG_ST(&part[kWgTM * kWgTN + wm + l32], bs0 + bx[(wq * 2) * 32 + l32]);
+      WG_ST(&part[kWgTM * kWgTN + wm + 32 + l32], bs1 + bx[(wq * 2 + 1) * 32 + l32]);
+    }
+  }
+  PSEC(9);
+}
+
 // Rows [kb0, kb1) of output tile tile_id into the partial tile `part` (+ the bias column sums
 // when the tile owns a bias column); an empty range writes a zero partial.
-__device__ __forceinline__ void wgrad_tile(const WgArgs& a, int tile_id, int kb0, int kb1,
+[[maybe_unused]] __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int tile_id, int kb0, int kb1,
                                            float* part, float* wg_lds PSEC_PARAMS) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, l32 = lane & 31;
   const int H = a.H;
@@ -2132,6 +2318,7 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int tile_id, int kb0
   // c + 1 (loaded during chunk c - 1) is staged
   f32x4 pa0[4], pb0[4], pa1[4], pb1[4];
   auto fetch = [&](int k0, f32x4(&pa)[4], f32x4(&pb)[4]) {
+    if (HWY_WG_EXP == 2 && k0 != kb0) return;
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       const uint32_t k = (uint32_t)min(k0 + 8 * w + 4 * ra + jj, kb1 - 1);
@@ -2199,10 +2386,15 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int tile_id, int kb0
       if (g + 1 < 4) rd(g + 1, b ^ 1);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
+        if (HWY_WG_EXP == 4) {
+          acc0[j] += x0[b][j] * y[b][j];
+          acc1[j] += x1[b][j] * y[b][j];
+          continue;
+        }
         acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(x0[b][j], y[b][j], acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(x1[b][j], y[b][j], acc1, 0, 0, 0);
       }
-      if constexpr (STASH) {
+      if constexpr (STASH && HWY_WG_EXP != 1) {
         piece(nA, nB, k_next, g, pa, pb);
         __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);  // the next group's operand reads
 #pragma unroll
@@ -2235,7 +2427,7 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int tile_id, int kb0
     } else {
       chunk(buf0, buf0 + kWgTM * 64, buf1, buf1 + kWgTM * 64, 0, pa1, pb1, no_stash);
     }
-    __syncthreads();
+    if (HWY_WG_EXP != 3) __syncthreads();
     if (c + 1 >= nchunk) break;
     // odd chunk c + 1 from buf1, chunk c + 2 (set 0) -> buf0, set 0 <- chunk c + 4
     if (c + 2 < nchunk) {
@@ -2245,7 +2437,7 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int tile_id, int kb0
     } else {
       chunk(buf1, buf1 + kWgTM * 64, buf0, buf0 + kWgTM * 64, 0, pa0, pb0, no_stash);
     }
-    __syncthreads();
+    if (HWY_WG_EXP != 3) __syncthreads();
   }
   PSEC(8);
   // waves 4-7 hand their accumulators to waves 0-3 through LDS (fixed order: even + odd groups)
@@ -2279,6 +2471,12 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int tile_id, int kb0
   PSEC(9);
 }
 
+#if HWY_WG_DMA
+#define WGRAD_TILE wgrad_tile_dma
+#else
+#define WGRAD_TILE wgrad_tile
+#endif
+
 // Workgroups.  Default: tile * split + z -> tile `tile`, row slice z (rows [z ceil(B / split),
 // ...)), then the head-sum workgroups.  Slice z goes to workgroups with id % 8 = z, i.e. to one
 // XCD (the dispatcher deals workgroups to the 8 XCDs round-robin), so each XCD reads one slice
@@ -2291,8 +2489,12 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int tile_id, int kb0
 // each slice also runs the head sums.
 __global__ void __launch_bounds__(512) ppo_wgrad(WgArgs a) {
   PSEC_DECL
-  __shared__ __attribute__((aligned(16))) float wg_lds[2 * (kWgTM + kWgTN) * 64];
-  __shared__ float red[kWgWaves];
+  // one LDS array (a second __shared__ object beside the LDS-DMA images can make the compiler
+  // drain every DMA before the first operand read of a chunk): the chunk buffers, then the
+  // reduction slots
+  constexpr int kWgBufs = HWY_WG_DMA ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) float wg_lds[kWgBufs * (kWgTM + kWgTN) * 64 + kWgWaves];
+  float* red = wg_lds + kWgBufs * (kWgTM + kWgTN) * 64;
   const int ntile = a.tac + a.t2 + a.t1;
   const int id = blockIdx.x;
   const int rows = (a.B + a.split - 1) / a.split;
@@ -2305,7 +2507,7 @@ __global__ void __launch_bounds__(512) ppo_wgrad(WgArgs a) {
     }
     const int z = id % a.split, tile = id / a.split;
     const int kb0 = z * rows, kb1 = min(a.B, kb0 + rows);
-    wgrad_tile(a, tile, kb0, kb1, a.slab + ((long)tile * a.split + z) * kWgPart,
+    WGRAD_TILE(a, tile, kb0, kb1, a.slab + ((long)tile * a.split + z) * kWgPart,
                wg_lds PSEC_ARGS);
     PSEC_FLUSH;
     return;
@@ -2316,13 +2518,13 @@ __global__ void __launch_bounds__(512) ppo_wgrad(WgArgs a) {
     return a.slab + (((long)tile * a.split + z) * a.nslot + sl) * kWgPart;
   };
   if (j < ntile) {
-    wgrad_tile(a, j, kz, km, slot(j, 0), wg_lds PSEC_ARGS);
+    WGRAD_TILE(a, j, kz, km, slot(j, 0), wg_lds PSEC_ARGS);
   } else {
     const int e = j - ntile, nextra = (int)gridDim.x / a.split - ntile;
     const int t0 = min(ntile, e * a.tpe), t1 = min(ntile, t0 + a.tpe);
     for (int tile = t0; tile < t1; ++tile) {
       if (tile > t0) __syncthreads();  // the last segment's accumulator exchange used the LDS
-      wgrad_tile(a, tile, km, kz1, slot(tile, 1), wg_lds PSEC_ARGS);
+      WGRAD_TILE(a, tile, km, kz1, slot(tile, 1), wg_lds PSEC_ARGS);
     }
     if (e == nextra - 1) {
       for (int hid = z; hid < a.nh; hid += a.split) {
