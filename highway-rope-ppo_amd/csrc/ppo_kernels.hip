@@ -31,8 +31,41 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // Development build only (make prof): shader-clock totals per phase of ppo_rows / ppo_wgrad,
 // summed over workgroups (wave 0), read back with hwy_ppo_debug_sections().
-#ifdef HWY_SECTION_PROFILE
+#if defined(HWY_SECTION_PROFILE) || defined(HWY_CLOCK_PROBE)
 __device__ unsigned long long g_ppo_sections[16];
+#endif
+// Development build only (HWY_CLOCK_PROBE): the in-kernel shader clock of ppo_rows* / ppo_wgrad,
+// as s_memtime (shader cycles) and s_memrealtime (100 MHz) deltas of thread 0 of every
+// workgroup, summed into g_ppo_sections[2k], [2k + 1] (k = 0 rows, 1 wgrad)
+#ifdef HWY_CLOCK_PROBE
+// also every workgroup's (start, end) s_memrealtime and HW_ID | XCC_ID << 32 of the last
+// launch of each kernel: g_ppo_wgt[k][blockIdx.x][3] (read with hwy_ppo_debug_wgtimes)
+__device__ unsigned long long g_ppo_wgt[2][1024][3];
+#define CLK_BEGIN                                         \
+  const uint64_t _c0 = __builtin_amdgcn_s_memtime();      \
+  const uint64_t _r0 = __builtin_amdgcn_s_memrealtime();
+#define CLK_END(k)                                                                   \
+  do {                                                                               \
+    if (threadIdx.x == 0) {                                                          \
+      const uint64_t _r1 = __builtin_amdgcn_s_memrealtime();                         \
+      atomicAdd(&g_ppo_sections[2 * (k)], __builtin_amdgcn_s_memtime() - _c0);       \
+      atomicAdd(&g_ppo_sections[2 * (k) + 1], _r1 - _r0);                            \
+      if (blockIdx.x < 1024) {                                                       \
+        g_ppo_wgt[k][blockIdx.x][0] = _r0;                                           \
+        g_ppo_wgt[k][blockIdx.x][1] = _r1;                                           \
+        g_ppo_wgt[k][blockIdx.x][2] =                                                \
+            (unsigned long long)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |  \
+            ((unsigned long long)(__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xff) << 32); \
+      }                                                                              \
+    }                                                                                \
+  } while (0)
+#else
+#define CLK_BEGIN
+#define CLK_END(k) \
+  do {             \
+  } while (0)
+#endif
+#ifdef HWY_SECTION_PROFILE
 #define PSEC_DECL                                \
   uint64_t _pt = __builtin_amdgcn_s_memtime();   \
   uint64_t _pacc[16];                            \
@@ -1402,7 +1435,9 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_rows(RowArgs r) {
 template <int QH, int NW, int RT>
 __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2 * NW / 4, 8)))
 ppo_rows_c(RowArgs r) {
+  CLK_BEGIN
   rows_body<QH, NW, RT, true>(r);
+  CLK_END(0);
 }
 
 // ----------------------------------------------------------------------------- ppo_rowsT
@@ -2487,7 +2522,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 // 256 / split - ntile "extras" take the other chunks of tpe tiles each (those chunks stay
 // L2-resident while an extra walks its tiles), into a second partial slot; the last extra of
 // each slice also runs the head sums.
-__global__ void __launch_bounds__(512) ppo_wgrad(WgArgs a) {
+__device__ __forceinline__ void ppo_wgrad_body(const WgArgs& a) {
   PSEC_DECL
   // one LDS array (a second __shared__ object beside the LDS-DMA images can make the compiler
   // drain every DMA before the first operand read of a chunk): the chunk buffers, then the
@@ -2535,6 +2570,12 @@ __global__ void __launch_bounds__(512) ppo_wgrad(WgArgs a) {
     }
   }
   PSEC_FLUSH;
+}
+
+__global__ void __launch_bounds__(512) ppo_wgrad(WgArgs a) {
+  CLK_BEGIN
+  ppo_wgrad_body(a);
+  CLK_END(1);
 }
 
 // ppo_wsum: the split partial tiles of every weight-gradient tile summed in split order
@@ -3168,7 +3209,12 @@ int hwy_ppo_build_flags(void) {
   return f;
 }
 
-#ifdef HWY_SECTION_PROFILE
+#ifdef HWY_CLOCK_PROBE
+int hwy_ppo_debug_wgtimes(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ppo_wgt), sizeof(g_ppo_wgt)) == hipSuccess ? 0 : -2;
+}
+#endif
+#if defined(HWY_SECTION_PROFILE) || defined(HWY_CLOCK_PROBE)
 int hwy_ppo_debug_sections(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ppo_sections), sizeof(g_ppo_sections)) != hipSuccess)
     return -2;
