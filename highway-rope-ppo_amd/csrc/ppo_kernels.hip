@@ -580,34 +580,49 @@ inline Work carve(const hwy_ppo_dims& d, void* ws, int64_t* bytes_out) {
   w.t1 = tmh * ((S + kWgTN - 1) / kWgTN);
   w.nh = (3 * H + 9 + 63) / 64;
   const int ntile = w.tac + w.t2 + w.t1;
-  // row slices per tile: one workgroup per CU, at least one 64-row chunk each, at most one per
-  // XCD, and a divisor of the XCD count (slice z = workgroup id % split then lands on the XCDs
-  // x with x % split == z under the dispatcher's round-robin placement -- for L2 locality only)
+  // Row slices per tile (split) and the balanced partition (ppo_wgrad).  Balanced: cus / split
+  // workgroups per slice when the tiles leave at least two CUs of each slice's share idle and
+  // the slices are long enough; the first wm chunks of every tile run on its own workgroup and
+  // the "extras" take the rest, tpe tiles each, paying ~1.5 chunks of pipeline fill per tile.
+  // The split is the largest divisor of the XCD count that gives every tile a workgroup (slice
+  // z = workgroup id % split then lands on the XCDs x with x % split == z under round-robin
+  // placement: each XCD's L2 serves one slice), unless another split's balanced partition
+  // shortens the critical path (64-row chunks per workgroup) by 15 % or more: 66 tiles at 32,768
+  // rows (H 384, S 240) run 3 slices at 138 chunks (332 us) instead of 2 at 172 (400 us; with
+  // tpe 2 half of the extras were idle).  (A 4-slice balanced partition of 32 tiles, H 256 /
+  // S 240, measured slower than 8 unbalanced slices: 186 against 164 us.)
   const ChipGeom chip = chip_geom();
-  {
-    const int cap = std::max(1, std::min({chip.xcds, 8, chip.cus / ntile, (B + 63) / 64}));
-    w.split = 1;
-    for (int sp = cap; sp >= 1; --sp)
-      if (chip.xcds % sp == 0) {
-        w.split = sp;
-        break;
-      }
-  }
-  w.grid2 = ntile * w.split + w.nh;
-  // balanced partition (ppo_wgrad): cus / split workgroups per slice when the tiles leave at
-  // least two CUs of each slice's share idle and the slices are long enough to split; an extra
-  // pays ~1.5 chunks of pipeline fill per tile
-  w.bal = 0, w.wm = 0, w.tpe = 0, w.nslot = 1;
-  {
-    const int P = chip.cus / w.split;                          // workgroups per slice
-    const int nck = ((B + w.split - 1) / w.split + 63) / 64;  // chunks of the longest slice
+  const double fill = dev_knob_double("HWY_WG_FILL", 1.5);
+  struct Plan {
+    int split, bal, wm, tpe, cost;
+  };
+  auto plan = [&](int sp) {
+    Plan q = {sp, 0, 0, 0, 0};
+    const int P = chip.cus / sp;                          // workgroups per slice
+    const int nck = ((B + sp - 1) / sp + 63) / 64;        // chunks of the longest slice
+    q.cost = nck;
     if (wg_balance_on() && ntile >= 16 && P - ntile >= 2 && nck >= 16) {
       const int E = P - ntile, tpe = (ntile + E - 1) / E;
-      const double fill = dev_knob_double("HWY_WG_FILL", 1.5);
       const int m = (int)std::ceil(tpe * (nck + fill) / (1.0 + tpe));
-      if (m < nck) w.bal = 1, w.wm = m, w.tpe = tpe, w.nslot = 2, w.grid2 = w.split * P;
+      if (m < nck) q.bal = 1, q.wm = m, q.tpe = tpe, q.cost = m;
     }
+    return q;
+  };
+  const int cap = std::max(1, std::min({chip.xcds, 8, chip.cus / ntile, (B + 63) / 64}));
+  Plan best = plan(1);
+  for (int sp = cap; sp >= 1; --sp)
+    if (chip.xcds % sp == 0) {
+      best = plan(sp);
+      break;
+    }
+  for (int sp = 2; sp <= std::min(8, std::max(1, (B + 63) / 64)); ++sp) {
+    if (chip.xcds % sp == 0) continue;
+    const Plan q = plan(sp);
+    if (q.bal && q.cost < 0.85 * best.cost && (!best.bal || q.cost < best.cost)) best = q;
   }
+  w.split = best.split;
+  w.bal = best.bal, w.wm = best.wm, w.tpe = best.tpe, w.nslot = best.bal ? 2 : 1;
+  w.grid2 = best.bal ? w.split * (chip.cus / w.split) : ntile * w.split + w.nh;
   w.nred2 = w.nh + ntile * (kWgTM * kWgTN / 1024);
   const int64_t head_rows = w.fused ? std::max<int64_t>(w.nhead, w.n1) : w.nhead;
   const int64_t norm_n = w.fused ? std::max(w.nred, w.nred2) : w.nred;
@@ -842,7 +857,10 @@ struct WSeg {
   int ldw, K, nblk, nn;  // nn: 0 W is [N][K], 1 W is [K][N] (k-major), 2 W is a tile image
 };
 
-template <int TW, int D, int NSEG, bool TL>
+// UNI: the tile-image block address is made wave-uniform (scalar base + one 32-bit lane offset);
+// it frees the VGPRs the compact ppo_rows needs to fit two workgroups per CU (141 -> 134 us at
+// 16,384 rows) but costs the 16-row kernels at H 384 (648 -> 686 us at 32,768 rows, S 240)
+template <int TW, int D, int NSEG, bool TL, bool UNI = false>
 struct WRing {
   f32x4 buf[D][TW];
   WSeg sg[NSEG];
@@ -854,13 +872,20 @@ struct WRing {
   __device__ __forceinline__ void load_blk(const float* W, int ldw, int nn, int kb,
                                            f32x4 (&dst)[TW]) {
     if constexpr (TL) {  // tile image (TileGeom): one contiguous KB per 16 columns and block
-      // wave-uniform tile address (scalar registers) + the lane's float4 (16 g + c = lane)
-      const int tile0 = __builtin_amdgcn_readfirstlane((n_base / 16) * ldw + (kb >> 4));
-      const float* p = W + (long)tile0 * 256;
-      const int lo = 4 * (16 * g + c);
+      if constexpr (UNI) {
+        // wave-uniform tile address (scalar registers) + the lane's float4 (16 g + c = lane)
+        const int tile0 = __builtin_amdgcn_readfirstlane((n_base / 16) * ldw + (kb >> 4));
+        const float* p = W + (long)tile0 * 256;
+        const int lo = 4 * (16 * g + c);
 #pragma unroll
-      for (int t = 0; t < TW; ++t)
-        dst[t] = *reinterpret_cast<const f32x4*>(p + (long)t * ldw * 256 + lo);
+        for (int t = 0; t < TW; ++t)
+          dst[t] = *reinterpret_cast<const f32x4*>(p + (long)t * ldw * 256 + lo);
+      } else {
+        const float* p = W + ((long)(n_base / 16) * ldw + (kb >> 4)) * 256 + (16 * g + c) * 4;
+#pragma unroll
+        for (int t = 0; t < TW; ++t)
+          dst[t] = *reinterpret_cast<const f32x4*>(p + (long)t * ldw * 256);
+      }
       return;
     }
     const int k = kb + 4 * g;
@@ -948,8 +973,8 @@ constexpr int ring_depth() { return TW <= 2 ? HWY_RING_D2 : (TW <= 4 ? 4 : 2); }
 // segment table of the row kernels: forward W1, W2, Wa1, Wc1 ([N][K]); backward Wa1, Wc1, W2
 // read k-major for dh2 = dac [Wa1; Wc1] and dh1 = dh2 W2.  With a tile image (TileGeom; kept by
 // hwy_ppo_sync_params / ppo_adam) every segment streams whole 1-KB tiles instead.
-template <int TW, int D, int NSEG, bool TL>
-__device__ __forceinline__ void ring_setup(WRing<TW, D, NSEG, TL>& R, const float* P,
+template <int TW, int D, int NSEG, bool TL, bool UNI>
+__device__ __forceinline__ void ring_setup(WRing<TW, D, NSEG, TL, UNI>& R, const float* P,
                                            const int64_t* off, int S, int H, int n_base,
                                            const float* tiles) {
   const int lane = threadIdx.x & 63;
@@ -1111,8 +1136,10 @@ __device__ __forceinline__ void rows_out(const float* img, int pitch, float* g, 
 // instead of going to AC, and the function ends without the barrier.
 // MSK: the ReLU decisions of h1 and h2 (this lane's C elements) also go to mb[0], mb[1] as bits
 // (row_epi_bias_relu_bits), so the backward needs neither image for its masks.
-template <int QH, int NW, int RT, bool KEEP, int D, int NSEG, bool TL, bool MSK = false>
-__device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG, TL>& R, const float* states,
+template <int QH, int NW, int RT, bool KEEP, int D, int NSEG, bool TL, bool MSK = false,
+          bool UNI = false>
+__device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG, TL, UNI>& R,
+                                             const float* states,
                                              const int64_t* idx, int S, int nrows, int row0,
                                              const float* P, const int64_t* off, float* X,
                                              float* H1, float* H2, float* AC, float* xg,
@@ -1231,7 +1258,7 @@ __device__ __forceinline__ void rows_body(const RowArgs& r) {
   const int nrows = min(RT, r.B - row0);
   const float* P = r.params;
   constexpr int D = CMP ? HWY_RING_DC : ring_depth<TW>();  // CMP: 4 waves per SIMD hide more
-  WRing<TW, D, 7, true> R;
+  WRing<TW, D, 7, true, CMP> R;
   ring_setup(R, P, r.off, S, H, w * (H / NW), r.tiles);
   R.prime();
   const int nb = w * (H / NW);  // this wave's output columns of an H-wide layer
