@@ -1072,7 +1072,14 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
 }
 
 // ------------------------------------------------------------------------- kernels
-__global__ void __launch_bounds__(256, 4) hwy_step_kernel(StepParams P) {
+// W: waves per SIMD the registers are sized for.  4 (106 VGPRs) when the envs fit one wave per
+// env on 4 waves per SIMD (4,096 envs on 256 CUs: 0.160 ms); 6 (80 VGPRs, 14 spilled to scratch
+// outside the hot loop) when more envs queue behind them: 16,384 envs 0.412 -> 0.365 ms,
+// 32,768 0.775 -> 0.670 (5 waves: 0.381 / 0.702), 8,192 0.228 -> 0.220; at 4,096 envs the 6-wave
+// build takes 0.164 ms, so hwy_launch_step picks by env count
+template <int W>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8)))
+hwy_step_kernel(StepParams P) {
   __shared__ int lds_vor[ENVS_PER_BLOCK][WAVE];
   __shared__ int lds_inv[ENVS_PER_BLOCK][WAVE];
   __shared__ CollLds lds_coll[ENVS_PER_BLOCK];
@@ -1284,9 +1291,32 @@ __global__ void hwy_math_kernel(int op, const float* in, const float* in2, float
 
 // ------------------------------------------------------------------------- launch helpers
 extern "C" {
+// compute units of the current device (cached per device; 256 without one)
+static int device_cus() {
+  static int cache[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    (void)hipGetLastError();
+    return 256;
+  }
+  if (!cache[dev]) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus < 1)
+      cus = 256;
+    (void)hipGetLastError();
+    cache[dev] = cus;
+  }
+  return cache[dev];
+}
+
 int hwy_launch_step(const StepParams* p, hipStream_t s) {
   const int blocks = (p->cfg.num_envs + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
-  hipLaunchKernelGGL(hwy_step_kernel, dim3(blocks), dim3(ENVS_PER_BLOCK * WAVE), 0, s, *p);
+  // one wave per env: more than 4 waves per SIMD of envs queue behind the first four
+  if ((int64_t)p->cfg.num_envs > (int64_t)16 * device_cus())
+    hipLaunchKernelGGL(hwy_step_kernel<6>, dim3(blocks), dim3(ENVS_PER_BLOCK * WAVE), 0, s, *p);
+  else
+    hipLaunchKernelGGL(hwy_step_kernel<4>, dim3(blocks), dim3(ENVS_PER_BLOCK * WAVE), 0, s, *p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int hwy_launch_reset(const StepParams* p, hipStream_t s) {
