@@ -1292,6 +1292,9 @@ __global__ void hwy_math_kernel(int op, const float* in, const float* in2, float
 // ------------------------------------------------------------------------- launch helpers
 extern "C" {
 // compute units of the current device (cached per device; 256 without one)
+#ifndef HWY_STEP_BIG_W
+#define HWY_STEP_BIG_W 6  // waves per SIMD the step kernel's registers are sized for at large E
+#endif
 static int device_cus() {
   static int cache[64] = {};
   int dev = 0;
@@ -1314,7 +1317,7 @@ int hwy_launch_step(const StepParams* p, hipStream_t s) {
   const int blocks = (p->cfg.num_envs + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
   // one wave per env: more than 4 waves per SIMD of envs queue behind the first four
   if ((int64_t)p->cfg.num_envs > (int64_t)16 * device_cus())
-    hipLaunchKernelGGL(hwy_step_kernel<6>, dim3(blocks), dim3(ENVS_PER_BLOCK * WAVE), 0, s, *p);
+    hipLaunchKernelGGL(hwy_step_kernel<HWY_STEP_BIG_W>, dim3(blocks), dim3(ENVS_PER_BLOCK * WAVE), 0, s, *p);
   else
     hipLaunchKernelGGL(hwy_step_kernel<4>, dim3(blocks), dim3(ENVS_PER_BLOCK * WAVE), 0, s, *p);
   return hipGetLastError() == hipSuccess ? 0 : -1;

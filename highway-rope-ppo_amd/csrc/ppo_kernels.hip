@@ -111,7 +111,8 @@ constexpr int kMaxRowS = 256;  // states dim bound of the fused path (LDS)
 #endif
 #ifndef HWY_WG_EXP
 // timing-only ppo_wgrad experiments (wrong results; development builds): 1 no LDS staging, 2 no
-// global loads after the first chunk, 3 no barriers in the chunk loop, 4 no MFMAs
+// global loads after the first chunk, 3 no barriers in the chunk loop, 4 no MFMAs, 5 (LDS-DMA
+// loop) no B-operand loads
 #define HWY_WG_EXP 0
 #endif
 #ifndef HWY_WG_DMA
@@ -2218,7 +2219,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
                                        (lds_void_t*)(buf + (4 * w + i) * 256), 16, 0, 0);
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < (HWY_WG_EXP == 5 ? 0 : 2); ++i) {
       const uint32_t row = (uint32_t)min(k0 + 4 * (2 * w + i) + rb, kb1 - 1);
       __builtin_amdgcn_global_load_lds((const void*)(Bm + (row * (uint32_t)ldb + b_col)),
                                        (lds_void_t*)(buf + kWgTM * 64 + (2 * w + i) * 256), 16,
@@ -2288,7 +2289,9 @@ typedef __attribute__((address_space(3))) void lds_void_t;
   auto step = [&](int c, auto mask_tag) {
     // this wave's pieces of chunk c landed (chunk c + 1's 6 may still be in flight) and its
     // reads of chunk c - 1 returned; after the barrier, every wave's
-    if (c + 1 < nchunk)
+    if (c + 1 < nchunk && HWY_WG_EXP == 5)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (c + 1 < nchunk)
       asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

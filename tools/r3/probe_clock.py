@@ -74,3 +74,10 @@ for k, name, nwg in ((0, "ppo_rows_c", mb // 32), (1, "ppo_wgrad", 269)):
         gaps = [abs(en[v[0]] - en[v[1]]) for v in grp.values() if len(v) == 2]
         if gaps:
             print(f"    end-time gap between a CU's two WGs: mean {np.mean(gaps):.1f} max {np.max(gaps):.1f} us")
+    if k == 1:  # balanced partition: id % 8 = slice, id / 8 = j; j < 26 main, then extras
+        j = np.arange(nwg)[a[k][:nwg, 1] > 0] // 8
+        for lab, m in (("main", j < 26), ("extras", (j >= 26) & (j < 31)), ("last extra (+head sums)", j == 31)):
+            if m.any():
+                print(f"    {lab:24s} n={m.sum():3d} start {st[m].mean():5.1f} lifetime mean {life[m].mean():5.1f} "
+                      f"max {life[m].max():5.1f} end max {en[m].max():5.1f} us")
+
