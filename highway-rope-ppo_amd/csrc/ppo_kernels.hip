@@ -1954,6 +1954,9 @@ struct ActArgs {
   const float* tiles;  // weight tile image in step with params (TL), else null
 };
 
+#ifndef HWY_ACT_CMP
+#define HWY_ACT_CMP 1  // ppo_act_c for large batches at H = 256 (0: always ppo_act)
+#endif
 #ifndef HWY_ACT_NW
 #define HWY_ACT_NW 8  // waves of ppo_act at H = 256 (development A/B)
 #endif
@@ -2032,6 +2035,100 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_act(ActArgs r) {
       r.value[b] = val;
     }
   }
+}
+
+// ppo_act_c: ppo_act for large batches at H = 256 in the compact layout of ppo_rows_c -- 32-row
+// tiles, the states / h1 / h2 images in two H-wide regions (P0 | P1, 71 KB with the head
+// partials), [a1 | c1] kept in the layer-3 accumulators, <= 128 VGPRs: two workgroups per CU.
+// The head is ppo_rows_c's: per-wave partial dot products of every row over the wave's columns,
+// summed in wave order, so mean / value are the bits the minibatch step recomputes.
+template <int QH, int NW, int RT>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2 * NW / 4, 8)))
+ppo_act_c(ActArgs r) {
+  constexpr int H = 64 * QH;
+  constexpr int TW = H / NW / 16;
+  constexpr int RB = RT / 16;
+  constexpr int RPW = RT / NW;
+  constexpr int PH = lds_pitch(H), PXMAX = lds_pitch(kMaxRowS);
+  static_assert(TW * 16 * NW == H && PXMAX <= PH && RPW >= 1 && RPW <= 16, "ppo_act_c geometry");
+  __shared__ __attribute__((aligned(16))) float P01[2 * RT * PH];
+  __shared__ __attribute__((aligned(16))) f32x4 HDOT[NW][RT];
+  float* const H1 = P01;            // P0
+  float* const P1 = P01 + RT * PH;  // the states, then h2
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int row0 = blockIdx.x * RT;
+  const int nrows = min(RT, r.B - row0);
+  const float* P = r.params;
+  constexpr int D = HWY_RING_DC;
+  WRing<TW, D, 4, true, true> R;
+  ring_setup(R, P, r.off, r.S, H, w * (H / NW), r.tiles);
+  R.prime();
+#ifdef HWY_SECTION_PROFILE
+  uint64_t _pt = 0, _pacc[16];
+#endif
+  float wa0[TW], wa1[TW], wc[TW];
+#pragma unroll
+  for (int u = 0; u < TW; ++u) {
+    const int col = w * (H / NW) + 16 * u + (lane & 15);
+    wa0[u] = P[r.off[P_WA2] + col];
+    wa1[u] = P[r.off[P_WA2] + H + col];
+    wc[u] = P[r.off[P_WC2] + col];
+  }
+  const float ba0 = P[r.off[P_BA2]], ba1 = P[r.off[P_BA2] + 1], bcv = P[r.off[P_BC2]];
+  const float ls0 = P[r.off[P_LOGSTD]], ls1 = P[r.off[P_LOGSTD] + 1];
+  // this lane's head row (lanes < RPW of wave w: row RPW w + lane) and its noise
+  const int hr = RPW * w + min(lane, RPW - 1);
+  const bool live = lane < RPW && hr < nrows;
+  const long b = row0 + min(hr, nrows - 1);
+  float n0 = 0.0f, n1 = 0.0f;
+  if (r.noise) n0 = r.noise[2 * b], n1 = r.noise[2 * b + 1];
+  f32x4 av[RB][TW], cv[RB][TW];
+  uint32_t mb[2] = {0u, 0u};
+  rows_forward<QH, NW, RT, true, D, 4, true, false>(R, r.states, nullptr, r.S, nrows, row0, P,
+                                                     r.off, P1, H1, P1, nullptr, nullptr,
+                                                     nullptr, nullptr, mb, av, cv PSEC_ARGS);
+  const int g4 = lane >> 4, c16 = lane & 15;
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float p0 = 0.0f, p1 = 0.0f, pv = 0.0f;
+#pragma unroll
+      for (int u = 0; u < TW; ++u) {
+        p0 += av[rb][u][q] * wa0[u];
+        p1 += av[rb][u][q] * wa1[u];
+        pv += cv[rb][u][q] * wc[u];
+      }
+      p0 = row16_sum(p0), p1 = row16_sum(p1), pv = row16_sum(pv);
+      if (c16 == 0) HDOT[w][16 * rb + 4 * g4 + q] = f32x4{p0, p1, pv, 0.0f};
+    }
+  __syncthreads();
+  if (!live) return;
+  f32x4 dsum = HDOT[0][hr];
+#pragma unroll
+  for (int ww = 1; ww < NW; ++ww) dsum += HDOT[ww][hr];
+  const float mu0 = dsum[0] + ba0, mu1 = dsum[1] + ba1, val = dsum[2] + bcv;
+  float z0 = mu0, z1 = mu1, lp = 0.0f;
+  if (r.noise) {
+    // torch Normal: scale = exp(log_std); var = scale**2; log_scale = log(scale)
+    const float sc0 = expf(ls0), sc1 = expf(ls1);
+    const float var0 = sc0 * sc0, var1 = sc1 * sc1;
+    const float lsc0 = logf(sc0), lsc1 = logf(sc1);
+    const float LOG_SQRT_2PI = 0.91893853320467274178f;
+    z0 = mu0 + sc0 * n0;
+    z1 = mu1 + sc1 * n1;
+    const float d0 = z0 - mu0, d1 = z1 - mu1;
+    const float t0 = tanhf(z0), t1 = tanhf(z1);
+    const float lp0 = -(d0 * d0) / (2.0f * var0) - lsc0 - LOG_SQRT_2PI;
+    const float lp1 = -(d1 * d1) / (2.0f * var1) - lsc1 - LOG_SQRT_2PI;
+    lp = (lp0 - log1pf(-(t0 * t0) + 1e-6f)) + (lp1 - log1pf(-(t1 * t1) + 1e-6f));
+  }
+  r.action[2 * b] = tanhf(z0);
+  r.action[2 * b + 1] = tanhf(z1);
+  r.pre_tanh[2 * b] = z0;
+  r.pre_tanh[2 * b + 1] = z1;
+  r.logp[b] = lp;
+  r.value[b] = val;
 }
 
 // ----------------------------------------------------------------------------- weight grads
@@ -3221,7 +3318,10 @@ int hwy_ppo_act(const hwy_ppo_act_args* a, void* stream) {
       default: hipLaunchKernelGGL((ppo_act<8, 8, TL>), g, b8, 0, s, r); break;
     }
   };
-  if (r.tiles)
+  // large batches at H = 256 (at least two 32-row tiles per CU): the compact two-per-CU kernel
+  if (HWY_ACT_CMP && r.tiles && d.H == 256 && d.B >= 64 * chip_geom().cus)
+    hipLaunchKernelGGL((ppo_act_c<4, 8, 32>), dim3((d.B + 31) / 32), b8, 0, s, r);
+  else if (r.tiles)
     launch(std::integral_constant<bool, true>());
   else
     launch(std::integral_constant<bool, false>());

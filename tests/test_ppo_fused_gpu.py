@@ -513,6 +513,49 @@ def test_fused_act_from_tile_image_equals_params_path(S, H):
         torch.testing.assert_close(g, r, rtol=1e-4, atol=2e-5)
 
 
+@pytest.mark.parametrize("S,B", [(60, 16384), (120, 20000)])
+def test_large_batch_act_kernel(S, B):
+    """ppo_act_c (H 256, at least two 32-row tiles per CU, tile image in step): against
+    ActorCritic.act with the same draws and against the 16-row kernel on the params path; and
+    its head is the minibatch step's, so re-evaluating the acted rows in a fused step gives a
+    ratio of exactly 1 on every row (KL and clip count exactly 0)."""
+    from hwy.ppo_native import fused_act
+
+    H, n = 256, 16384
+    a, b = _agents(S, H)
+    s, z, lp, adv, ret, perm = _data(n, S, a)
+    F = FusedPPO(b, n, 1, use_graphs=False)
+    b._fused = F
+    F.run(s, z, lp, adv.clone(), ret.clone(), perm.clone())  # the tile image follows params now
+    assert F.current_tiles(F.flat) is not None
+    a.actor_critic.load_state_dict(b.actor_critic.state_dict())
+    x = torch.randn(B, S, device=DEV)
+    gen = lambda: torch.Generator(device=DEV).manual_seed(7)  # noqa: E731
+    with torch.no_grad():
+        ref = a.actor_critic.act(x, generator=gen())
+        got = fused_act(b, x, generator=gen())
+        saved = F._tiles_version
+        F._tiles_version = None  # the 16-row kernel from the flat params
+        got_p = fused_act(b, x, generator=gen())
+        F._tiles_version = saved
+        got_d = fused_act(b, x, deterministic=True)
+        ref_d = a.actor_critic.act(x, deterministic=True)
+    for r, g, p_ in zip(ref, got, got_p):
+        torch.testing.assert_close(g, r, rtol=1e-4, atol=2e-5)
+        torch.testing.assert_close(g, p_, rtol=1e-4, atol=2e-5)
+    for r, g in zip(ref_d, got_d):
+        torch.testing.assert_close(g, r, rtol=1e-4, atol=2e-5)
+    if B == n:
+        _, pre, logp, _ = got
+        idx = torch.arange(n, device=DEV, dtype=torch.int64)
+        args = F._args(x, pre.contiguous(), logp.contiguous(), adv, ret, idx.data_ptr())
+        F.counters.zero_()
+        F._fwd_bwd(args)
+        torch.cuda.synchronize()
+        m = F.metrics[0]
+        assert m[4].item() == 0.0 and m[5].item() == 0.0, m.tolist()
+
+
 def test_rollout_noise_value_and_dones_helpers():
     """Pre-drawn rollout noise (RolloutBuffer.draw_noise, one draw per rollout) gives the same
     sample through the kernel and ActorCritic.act; agent.value is the critic's V(s);
