@@ -1955,7 +1955,7 @@ struct ActArgs {
 };
 
 #ifndef HWY_ACT_CMP
-#define HWY_ACT_CMP 1  // ppo_act_c for large batches at H = 256 (0: always ppo_act)
+#define HWY_ACT_CMP 1  // ppo_act_c at H = 256 from the tile image (0: always ppo_act)
 #endif
 #ifndef HWY_ACT_NW
 #define HWY_ACT_NW 8  // waves of ppo_act at H = 256 (development A/B)
@@ -2037,9 +2037,9 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_act(ActArgs r) {
   }
 }
 
-// ppo_act_c: ppo_act for large batches at H = 256 in the compact layout of ppo_rows_c -- 32-row
-// tiles, the states / h1 / h2 images in two H-wide regions (P0 | P1, 71 KB with the head
-// partials), [a1 | c1] kept in the layer-3 accumulators, <= 128 VGPRs: two workgroups per CU.
+// ppo_act_c: ppo_act at H = 256 in the compact layout of ppo_rows_c -- the states / h1 / h2
+// images in two H-wide regions (P0 | P1: 71 KB with the head partials at 32-row tiles, 36 KB at
+// 16), [a1 | c1] kept in the layer-3 accumulators, <= 128 VGPRs: two workgroups per CU.
 // The head is ppo_rows_c's: per-wave partial dot products of every row over the wave's columns,
 // summed in wave order, so mean / value are the bits the minibatch step recomputes.
 template <int QH, int NW, int RT>
@@ -3318,10 +3318,14 @@ int hwy_ppo_act(const hwy_ppo_act_args* a, void* stream) {
       default: hipLaunchKernelGGL((ppo_act<8, 8, TL>), g, b8, 0, s, r); break;
     }
   };
-  // large batches at H = 256 (at least two 32-row tiles per CU): the compact two-per-CU kernel
-  if (HWY_ACT_CMP && r.tiles && d.H == 256 && d.B >= 64 * chip_geom().cus)
-    hipLaunchKernelGGL((ppo_act_c<4, 8, 32>), dim3((d.B + 31) / 32), b8, 0, s, r);
-  else if (r.tiles)
+  // H = 256 from the tile image: the compact kernel, 32-row tiles once there are two per CU
+  // (16,384 rows on MI355X: 91.3 -> 69.4 us), else 16-row tiles (4,096 rows: 25.1 -> 22.0 us)
+  if (HWY_ACT_CMP && r.tiles && d.H == 256) {
+    if (d.B >= 64 * chip_geom().cus)
+      hipLaunchKernelGGL((ppo_act_c<4, 8, 32>), dim3((d.B + 31) / 32), b8, 0, s, r);
+    else
+      hipLaunchKernelGGL((ppo_act_c<4, 8, 16>), dim3((d.B + 15) / 16), b8, 0, s, r);
+  } else if (r.tiles)
     launch(std::integral_constant<bool, true>());
   else
     launch(std::integral_constant<bool, false>());

@@ -482,8 +482,9 @@ def test_fused_act_matches_actor_critic_act(S, H, B):
 @pytest.mark.parametrize("S,H", [(60, 256), (120, 192)])
 def test_fused_act_from_tile_image_equals_params_path(S, H):
     """After a fused update the acting kernel streams the update's weight tile image
-    (hwy_ppo_tile_image_offset); results are bit-identical to reading the flat params, and a
-    torch-side parameter write (load_state_dict) retires the image until the next update."""
+    (hwy_ppo_tile_image_offset); results are bit-identical to reading the flat params (at
+    H = 256 the image path is the compact kernel and agrees to fp32 rounding), and a torch-side
+    parameter write (load_state_dict) retires the image until the next update."""
     from hwy.ppo_native import fused_act
 
     a, b = _agents(S, H)
@@ -502,7 +503,10 @@ def test_fused_act_from_tile_image_equals_params_path(S, H):
         got_p = fused_act(b, x, generator=torch.Generator(device=DEV).manual_seed(5))
         F._tiles_version = saved
     for t_, p_ in zip(got_t, got_p):
-        assert torch.equal(t_, p_)
+        if H == 256:  # ppo_act_c (register head) against ppo_act: fp32 agreement
+            torch.testing.assert_close(t_, p_, rtol=1e-4, atol=2e-5)
+        else:  # the same kernel on both paths: bit-identical
+            assert torch.equal(t_, p_)
     # a torch-side write bumps the flat buffer's version: acting falls back to params
     b.actor_critic.load_state_dict(a.actor_critic.state_dict())
     assert F.current_tiles(flat) is None
@@ -513,15 +517,15 @@ def test_fused_act_from_tile_image_equals_params_path(S, H):
         torch.testing.assert_close(g, r, rtol=1e-4, atol=2e-5)
 
 
-@pytest.mark.parametrize("S,B", [(60, 16384), (120, 20000)])
-def test_large_batch_act_kernel(S, B):
-    """ppo_act_c (H 256, at least two 32-row tiles per CU, tile image in step): against
-    ActorCritic.act with the same draws and against the 16-row kernel on the params path; and
-    its head is the minibatch step's, so re-evaluating the acted rows in a fused step gives a
-    ratio of exactly 1 on every row (KL and clip count exactly 0)."""
+@pytest.mark.parametrize("S,B", [(60, 16384), (120, 20000), (60, 4096), (120, 1000)])
+def test_compact_act_kernel(S, B):
+    """ppo_act_c (H 256, tile image in step; 32-row tiles from two per CU, else 16): against
+    ActorCritic.act with the same draws and against ppo_act on the params path; and its head is
+    the minibatch step's, so re-evaluating the acted rows in a fused step gives a ratio of
+    exactly 1 on every row (KL and clip count exactly 0)."""
     from hwy.ppo_native import fused_act
 
-    H, n = 256, 16384
+    H, n = 256, min(B, 16384)
     a, b = _agents(S, H)
     s, z, lp, adv, ret, perm = _data(n, S, a)
     F = FusedPPO(b, n, 1, use_graphs=False)
