@@ -12,7 +12,8 @@ from hwy.ppo_native import FusedPPO, fused_act
 from ppo.agent import PPOAgent
 
 dev = torch.device("cuda", 0)
-S, H, n = 60, 256, 16384
+S, H = (int(v) for v in os.environ.get("HWY_PROBE_SH", "60:256").split(":"))
+n = 16384
 torch.manual_seed(0)
 ag = PPOAgent(S, 2, lr=3e-4, epochs=1, hidden_dim=H, device=dev, use_graphs=False, backend="hip")
 s = torch.randn(n, S, device=dev); z = torch.randn(n, 2, device=dev)
