@@ -484,10 +484,17 @@ __device__ void observe_wave(const hwy_config& C, int lane, const Veh& v, float 
   if (C.order == HWY_ORDER_SORTED) {
     float key = hm_absf(v.x - ex);
     rank = 0;
-    for (int k = 1; k < V; ++k) {
-      if (!((em >> k) & 1ull)) continue;
-      float kk = rdlf(key, k);
-      if (kk < key || (kk == key && k < lane)) ++rank;
+    // four vehicles per round: their keys are read first, then compared (no branch per vehicle)
+    for (int k0 = 1; k0 < V; k0 += 4) {
+      float kk[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) kk[u] = rdlf(key, min(k0 + u, WAVE - 1));
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + u;
+        const bool ek = k < V && ((em >> k) & 1ull);
+        rank += (ek && (kk[u] < key || (kk[u] == key && k < lane))) ? 1 : 0;
+      }
     }
   } else {
     rank = __popcll(em & ((1ull << lane) - 1ull));
@@ -504,9 +511,15 @@ __device__ void observe_wave(const hwy_config& C, int lane, const Veh& v, float 
                              (uint32_t)(seed & 0xffffffffu), (uint32_t)(seed >> 32))
                 .v[0];
     int dest = 0;
-    for (int p = 0; p < N - 1; ++p) {
-      uint32_t kp = (uint32_t)rdli((int)key, p);
-      if (kp < key || (kp == key && p < lane)) ++dest;
+    for (int p0 = 0; p0 < N - 1; p0 += 4) {
+      uint32_t kp[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) kp[u] = (uint32_t)rdli((int)key, min(p0 + u, WAVE - 1));
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int p = p0 + u;
+        dest += (p < N - 1 && (kp[u] < key || (kp[u] == key && p < lane))) ? 1 : 0;
+      }
     }
     if (lane < N - 1) lds_inv[dest] = lane;
   }
