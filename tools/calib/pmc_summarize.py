@@ -1,7 +1,8 @@
 """Calibrated hwy_step HBM bytes per launch from the pmc_step.sh passes
     python3 tools/calib/pmc_summarize.py <dir> [E N F_out]
 -> profiles/hwy_step_pmc.json (E 4096, N 15, F_out 4) or profiles/hwy_step_pmc_E<E>_N<N>_F<F>.json"""
-import csv, glob, json, os, sys
+import csv
+import re, glob, json, os, sys
 
 d = sys.argv[1]
 E = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
@@ -17,7 +18,8 @@ def per_kernel(pass_dir, counter):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            name = r["Kernel_Name"].split("(")[0]
+            # "void hwy_step_kernel<4>(StepParams)" -> "hwy_step_kernel"
+            name = re.sub(r"<.*>", "", r["Kernel_Name"].split("(")[0]).replace("void ", "").strip()
             out.setdefault(name, []).append(float(r["Counter_Value"]) * 1024.0)  # KiB -> B
     return {k: sum(v[1:]) / max(1, len(v) - 1) if len(v) > 1 else v[0] for k, v in out.items()}
 

@@ -40,4 +40,4 @@ cd $R
 python3 tools/calib/pmc_summarize.py $O $E $N $F > /dev/null && \
 python3 tools/calib/valu_summarize.py $O/valu $N $F > /dev/null && \
 python3 tools/calib/ppo_traffic_summarize.py $O/ppo $MB $S $H | grep hbm_side
-ls -1 profiles/*E${E}_N${N}* profiles/ppo_step_pmc_${MB}_S${S}_H${H}.json
+ls -1 profiles/*E${E}_N${N}* profiles/ppo_step_pmc_${MB}_S${S}_H${H}.json || true  # (written where the summaries run; gpurun merges only gpurun_out/)
