@@ -103,7 +103,9 @@ HWY_HD float hm_sincos_core(float xx, int want_cos) {
     x = -x;
     if (!want_cos) sign = -1;
   }
-  if (!(x <= 16777215.0f)) return hm_isnan(x) ? x : 0.0f; /* total loss of precision */
+  /* |x| >= 2^24: total loss of precision, Cephes returns 0; x - x keeps that for finite x and
+   * gives NaN for inf and NaN, as libm / numpy do */
+  if (!(x <= 16777215.0f)) return x - x;
   uint32_t j = (uint32_t)(FOPI * x);
   float y = (float)j;
   if (j & 1u) {
@@ -147,7 +149,7 @@ HWY_HD void hm_sincosf(float xx, float* s_out, float* c_out) {
     sign_s = -1;
   }
   if (!(x <= 16777215.0f)) {
-    const float r = hm_isnan(x) ? x : 0.0f;
+    const float r = x - x; /* as hm_sincos_core */
     *s_out = r;
     *c_out = r;
     return;
