@@ -468,7 +468,7 @@ struct Work {
   float *wtile;              // fused: weight tile image (TileGeom)
   int nhead, HP, sa, s2, s1, ca, c2, c1, nred;
   // fused path (ppo_rows + ppo_wgrad)
-  bool fused, rows_t;  // rows_t: ppo_rowsT (64 rows per workgroup) instead of ppo_rows
+  bool fused;
   int rt, n1, tac, t2, t1, nh, split, grid2, nred2;  // rt: rows per ppo_rows workgroup
   int bal, wm, tpe, nslot;                            // ppo_wgrad's balanced partition
   int sb, hb;  // ring blocks of the row kernels (rows_blocks)
@@ -541,15 +541,6 @@ inline bool fused_ok(const hwy_ppo_dims& d) {
 
 inline int head_stride(int H) { return 3 * H + 16; }
 
-// ppo_rowsT (the transposed row kernel, 64 rows per workgroup) where the minibatch gives every
-// CU a workgroup (H <= 256, B a multiple of 64, B >= 64 x CUs).  Measured slower than ppo_rows
-// (146 against 125 us at 16,384 rows), so only a development build selects it (HWY_ROWS_T=1).
-constexpr int kTRowsWG = 64;
-inline bool rows_t_ok(const hwy_ppo_dims& d) {
-  return fused_ok(d) && d.H <= 256 && d.B % kTRowsWG == 0 &&
-         (int64_t)d.B >= (int64_t)kTRowsWG * chip_geom().cus &&
-         dev_knob_int("HWY_ROWS_T", 0) != 0;
-}
 constexpr int kRedThreads = 256;
 
 inline Work carve(const hwy_ppo_dims& d, void* ws, int64_t* bytes_out) {
@@ -572,8 +563,7 @@ inline Work carve(const hwy_ppo_dims& d, void* ws, int64_t* bytes_out) {
   const Layout L = make_layout(d);
   w.nred = (int)((L.numel + kRedThreads - 1) / kRedThreads);
   w.fused = fused_ok(d);
-  w.rows_t = w.fused && rows_t_ok(d);
-  w.rt = w.rows_t ? kTRowsWG : rows_tile(B, H);
+  w.rt = rows_tile(B, H);
   w.n1 = (B + w.rt - 1) / w.rt;
   const int tmh = (H + kWgTM - 1) / kWgTM, tnh = (H + kWgTN - 1) / kWgTN;
   w.tac = ((2 * H + kWgTM - 1) / kWgTM) * tnh;
@@ -1466,478 +1456,6 @@ ppo_rows_c(RowArgs r) {
   CLK_BEGIN
   rows_body<QH, NW, RT, true>(r);
   CLK_END(0);
-}
-
-// ----------------------------------------------------------------------------- ppo_rowsT
-// The row-local part of the minibatch step (the same outputs as ppo_rows) in the transposed
-// formulation, for minibatches of at least 64 rows per CU (the bench's 16,384- and 32,768-row
-// minibatches at H <= 256).  One 256-thread workgroup = 4 waves x 16 rows; each wave computes
-// every layer of its own 16 rows as out^T[feature][row] = W . in^T:
-//   v_mfma_f32_16x16x4_f32 with A = a 16 x 16 weight tile (M = output features, K = inputs) and
-//   B = the wave's activations (K = inputs, N = its 16 rows).  The C fragment of output block G
-//   (lane (c, g) reg r = feature 16G + 4g + r of row c) is exactly the B fragment of k-block G of
-//   the next layer (sub-step j of lane (c, g) uses k = 4g + j), so a layer's output never has to
-//   be re-laid out: the forward keeps a1 / c1 and the loss head keeps dac in registers, and the
-//   backward's dh2 = [Wa1; Wc1]^T dac streams its B operand straight from them.
-// The weights stream once per workgroup through a two-slot LDS ring shared by the 4 waves, one
-// "stage" of 2 NG 1-KB tiles (NG = H / 16) per barrier: forward / dh1 layers 2 k-blocks x NG
-// output blocks, layer 3 one k-block of Wa1 and Wc1, dh2 (NG / 2) k-blocks x 4 output blocks.
-// Tiles come from the same tile image as ppo_rows (TileGeom; A fragment = lane's float4 of the
-// 1-KB tile).  Stage i + 1's tiles are loaded to registers during stage i - 1 and written to the
-// ring at the start of stage i.  Each wave's input activations sit in a private LDS row image
-// (x, then h1 / h2 / dh2 in place) read as B fragments with ds_read_b128.
-constexpr int kTRows = kTRowsWG;  // minibatch rows per ppo_rowsT workgroup (4 waves x 16)
-
-// Tile (w + 4q) of stage i of ppo_rowsT's weight stream, for the thread's wave w: an affine
-// function of q in at most two pieces (tile index = q < qs ? b0 + q s0 : b1 + (q - qs) s1, in
-// 1-KB tiles of the image).  Stages: layer 1 (sb / 2), layer 2 (NG / 2), layer 3 (NG), dh2
-// (NG), dh1 (NG / 2); tile t of a stage is read from ring position t.
-struct RtDesc {
-  int b0, s0, b1, s1, qs;
-};
-template <int NG>
-__device__ __forceinline__ RtDesc rt_desc(const TileGeom& T, int sb, int i, int w) {
-  constexpr int hb = NG, NQ = NG / 2;
-  const int n1 = sb / 2, n2 = NG / 2, n3 = NG, n4 = NG, n5 = NG / 2;
-  RtDesc d = {0, 0, 0, 0, NQ};
-  // k-outer layers: t = 2G + kk -> tile (G, 2 i + kk) = base + (w >> 1 + 2q) nblk + 2i + (w & 1)
-  auto kouter = [&](int64_t img, int nblk, int ii) {
-    d.b0 = (int)(img / 256) + (w >> 1) * nblk + 2 * ii + (w & 1);
-    d.s0 = 2 * nblk;
-  };
-  if (i < n1) {
-    kouter(T.f1, sb, i);
-  } else if ((i -= n1) < n2) {
-    kouter(T.f2, hb, i);
-  } else if ((i -= n2) < n3) {  // t < NG: Wa1 tile (t, i); else Wc1 tile (t - NG, i)
-    d.b0 = (int)(T.fa / 256) + w * hb + i, d.s0 = 4 * hb;
-    d.b1 = (int)(T.fc / 256) + w * hb + i, d.s1 = 4 * hb, d.qs = NG / 4;
-  } else if ((i -= n3) < n4) {  // t = 4 kl + u -> output block 4 (i / 4) + u, k-block (NG/2)(i%4) + kl
-    const int G = 4 * (i >> 2) + w, ls = i & 3;
-    const int64_t img = ls < 2 ? T.ba : T.bc;  // K = 2H: actor rows, then critic rows
-    d.b0 = (int)(img / 256) + G * hb + NQ * (ls & 1), d.s0 = 1;
-  } else if ((i -= n4) < n5) {
-    kouter(T.b2, hb, i);
-  } else {
-    d.s0 = 0;  // past the end: tile 0 (loaded, never read)
-  }
-  return d;
-}
-
-// The schedule as a table of tile indices, [stage][wave][q], built once per workgroup in LDS
-// (the stage loops then issue their loads without re-deriving the phase)
-constexpr int kRtMaxStages = 64;  // sb / 2 + 3 NG + 2 <= 8 + 48 + 2
-
-template <int NG>
-struct RtRing {
-  static constexpr int STG = 2 * NG;  // tiles per stage
-  static constexpr int NQ = NG / 2;   // float4 per thread per stage (STG * 64 / 256)
-  f32x4 st[NQ];
-  int nxt[NQ];       // tile indices of the next stage to load (read one stage ahead)
-  float* lds;        // 2 slots x STG x 256 floats
-  const int* sched;  // [kRtMaxStages][4][NQ] tile indices
-  const float* tiles;
-  static __device__ void build(int* sched, const TileGeom& T, int sb) {
-    const int nst = sb / 2 + 3 * NG;
-    for (int e = threadIdx.x; e < (nst + 2) * 4 * NQ; e += blockDim.x) {
-      const int i = e / (4 * NQ), w = (e / NQ) & 3, q = e % NQ;
-      const RtDesc d = rt_desc<NG>(T, sb, i, w);
-      sched[e] = q < d.qs ? d.b0 + q * d.s0 : d.b1 + (q - d.qs) * d.s1;
-    }
-  }
-  __device__ __forceinline__ void read_sched(int i) {
-    const int* tl = sched + (i * 4 + (threadIdx.x >> 6)) * NQ;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) nxt[q] = tl[q];
-  }
-  // stage i's loads (its indices were read by the previous load), then stage i + 1's indices
-  __device__ __forceinline__ void load(int i) {
-    const float* src = tiles + 4 * (threadIdx.x & 63);
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int tile = __builtin_amdgcn_readfirstlane(nxt[q]);
-      st[q] = *reinterpret_cast<const f32x4*>(src + (int64_t)tile * 256);
-    }
-    read_sched(i + 1);
-  }
-  __device__ __forceinline__ void store(int i) {
-    float* dst = lds + (i & 1) * STG * 256 + (threadIdx.x >> 6) * 256 + 4 * (threadIdx.x & 63);
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) *reinterpret_cast<f32x4*>(dst + q * 4 * 256) = st[q];
-  }
-  // start of stage i (the barrier that ended stage i - 1 has passed): stage i + 1's tiles (in
-  // registers) into their slot -- stage i - 1's, which every wave has finished reading -- and
-  // stage i + 2's loads issued
-  __device__ __forceinline__ void advance(int i) {
-    store(i + 1);
-    load(i + 2);
-  }
-  __device__ __forceinline__ const float* slot(int i) const {
-    return lds + (i & 1) * STG * 256 + 4 * (threadIdx.x & 63);
-  }
-};
-
-// Selects in integer VALU ops (no compare masks, which the compiler keeps in SGPR pairs and
-// spills when dozens are live): relu output r (+0 or positive) on ? v : +0, and bit b of m ? v : +0
-__device__ __forceinline__ float sel_on(float relu_out, float v) {
-  const uint32_t on = (__float_as_uint(relu_out) + 0x7fffffffu) >> 31;
-  return __uint_as_float(__float_as_uint(v) & (0u - on));
-}
-__device__ __forceinline__ float sel_bit(uint32_t m, int b, float v) {
-  return __uint_as_float(__float_as_uint(v) & (0u - ((m >> b) & 1u)));
-}
-
-// the two fragments' four k sub-steps interleaved over two accumulators (dependent MFMAs two
-// issues apart: 64 cycles > the 40-cycle accumulator latency)
-__device__ __forceinline__ void mfma4x2(const f32x4& a0, const f32x4& a1, const f32x4& b0,
-                                        const f32x4& b1, f32x4& c0, f32x4& c1) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[j], b0[j], c0, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[j], b1[j], c1, 0, 0, 0);
-  }
-}
-
-// A software-pipelined sequence of NSTEP steps: step s reads K LDS fragments (rd(s, frag)) and
-// issues its MFMAs (mm(s, frag)); step s + 1's reads are issued before step s's MFMAs and the
-// order is pinned (one wave per SIMD: nothing else hides an LDS read's latency).
-template <int NSTEP, int K, class RD, class MM>
-__device__ __forceinline__ void rt_piped(RD rd, MM mm) {
-  f32x4 cur[K], nxt[K];
-  rd(0, cur);
-#pragma unroll
-  for (int s = 0; s < NSTEP; ++s) {
-    if (s + 1 < NSTEP) rd(s + 1, nxt);
-    __builtin_amdgcn_sched_barrier(0);
-    mm(s, cur);
-    __builtin_amdgcn_sched_barrier(0);
-    if (s + 1 < NSTEP) {
-#pragma unroll
-      for (int k = 0; k < K; ++k) cur[k] = nxt[k];
-    }
-  }
-}
-
-__device__ __forceinline__ f32x4 lds4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
-
-// nst stages of 2 k-blocks each: acc[G] += tiles (G, 2 ls + kk) x act k-block 2 ls + kk, the
-// act fragments read from the wave's row image (lane (c, g): row c, k = 16 kb + 4 g .. + 3)
-template <int NG, int SEC>
-__device__ __forceinline__ void rt_kouter(RtRing<NG>& R, int& i, int nst, const float* brow,
-                                          f32x4 (&acc)[NG] PSEC_PARAMS) {
-  for (int ls = 0; ls < nst; ++ls, ++i) {
-    R.advance(i);
-    const float* sl = R.slot(i);
-    const float* bp = brow + 32 * ls;
-    // step s: k-block kk = s / (NG/2), output blocks 2p, 2p + 1 (p = s % (NG/2)); fragment 2 is
-    // the act k-block (re-read per step: a broadcast-free 16-B read, cheap beside 8 MFMAs)
-    rt_piped<NG, 3>(
-        [&](int st, f32x4(&f)[3]) {
-          const int kk = st / (NG / 2), p = st % (NG / 2);
-          f[0] = lds4(sl + (4 * p + kk) * 256);
-          f[1] = lds4(sl + (4 * p + 2 + kk) * 256);
-          f[2] = lds4(bp + 16 * kk);
-        },
-        [&](int st, const f32x4(&f)[3]) {
-          const int p = st % (NG / 2);
-          mfma4x2(f[0], f[1], f[2], f[2], acc[2 * p], acc[2 * p + 1]);
-        });
-    PSEC(SEC);
-    __syncthreads();
-    PSEC(12);
-  }
-}
-
-template <int QH>
-__global__ void __launch_bounds__(256, 1) ppo_rowsT(RowArgs r) {
-  constexpr int H = 64 * QH, NG = H / 16;
-  static_assert(NG % 4 == 0, "ppo_rowsT: H a multiple of 64");
-  constexpr int STG = 2 * NG;
-  constexpr int kXMax = kMaxRowS > H ? kMaxRowS : H;
-  constexpr int PW = lds_pitch(kXMax);  // row image pitch (conflict-free B fragment reads)
-  // LDS: the ring, 4 row images, the head's weight rows and the layer biases
-  constexpr int L_RING = 2 * STG * 256, L_ACT = 4 * 16 * PW, L_HW = 3 * H, L_B = 4 * H;
-  constexpr int L_SCHED = kRtMaxStages * 4 * (NG / 2);
-  __shared__ __attribute__((aligned(16))) float lds[L_RING + L_ACT + L_HW + L_B + L_SCHED];
-  float* ring = lds;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, g = lane >> 4, c = lane & 15;
-  float* act = lds + L_RING + w * 16 * PW;  // this wave's 16 rows
-  float* hw = lds + L_RING + L_ACT;         // wa2 row 0, row 1, wc2
-  float* lb = hw + L_HW;                    // b1, b2, ba1, bc1
-  const int S = r.S;
-  const float* P = r.params;
-  const int sb = ((S + 15) / 16 + 3) / 4 * 4;  // k-blocks of layer 1 (the image's, rows_blocks)
-  const int Sp = 16 * sb;
-  const int row0 = blockIdx.x * kTRows + 16 * w;  // this wave's first minibatch row
-  const int myrow = row0 + c;
-  RtRing<NG> R;
-  R.lds = ring;
-  R.tiles = r.tiles;
-  int* sched = reinterpret_cast<int*>(lb + L_B);
-  R.sched = sched;
-  RtRing<NG>::build(sched, tile_geom(S, H, sb, NG), sb);
-  __syncthreads();
-  R.read_sched(0);
-  R.load(0);
-  // head weights and biases to LDS, the row's loss inputs to registers
-  for (int e = t; e < H; e += 256) {
-    hw[e] = P[r.off[P_WA2] + e];
-    hw[H + e] = P[r.off[P_WA2] + H + e];
-    hw[2 * H + e] = P[r.off[P_WC2] + e];
-    lb[e] = P[r.off[P_B1] + e];
-    lb[H + e] = P[r.off[P_B2] + e];
-    lb[2 * H + e] = P[r.off[P_BA1] + e];
-    lb[3 * H + e] = P[r.off[P_BC1] + e];
-  }
-  const long src_row = (long)r.idx[myrow];
-  const float hz0 = r.pre_tanh[src_row * 2], hz1 = r.pre_tanh[src_row * 2 + 1];
-  const float hq0 = log1pf(-(tanhf(hz0) * tanhf(hz0)) + 1e-6f);
-  const float hq1 = log1pf(-(tanhf(hz1) * tanhf(hz1)) + 1e-6f);
-  const float hold = r.old_logp[src_row], hadv = r.adv[src_row], hret = r.ret[src_row];
-  const float ba0 = P[r.off[P_BA2]], ba1 = P[r.off[P_BA2] + 1], bcv = P[r.off[P_BC2]];
-  const float ls0 = P[r.off[P_LOGSTD]], ls1 = P[r.off[P_LOGSTD] + 1];
-  // the wave's states rows, zero-padded to Sp columns, also to xg (ppo_wgrad's dW1 operand)
-  for (int e = lane; e < 16 * (Sp / 4); e += 64) {
-    const int rr = e / (Sp / 4), k = 4 * (e % (Sp / 4));
-    f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (k < S) {
-      const long src = (long)r.idx[row0 + rr];
-      v = *reinterpret_cast<const f32x4*>(r.states + src * S + k);
-      *reinterpret_cast<f32x4*>(r.xg + (long)(row0 + rr) * S + k) = v;
-    }
-    *reinterpret_cast<f32x4*>(&act[rr * PW + k]) = v;
-  }
-  R.store(0);
-  R.load(1);
-  __syncthreads();
-  const float* brow = act + c * PW + 4 * g;  // B fragments of the row image
-  float* arow = act + c * PW + 4 * g;        // C fragments written back (same positions)
-  int i = 0;
-  PSEC_DECL
-  PSEC(0);
-  f32x4 acc[NG];
-  // ReLU masks of h1 / h2 as VGPR bit sets (bit 4G + r of word (4G + r) / 32), built with
-  // integer VALU ops only: relu(x) is +0 or a positive float, so bits(v) != 0 <=> x > 0
-  uint32_t m1[(NG + 7) / 8], m2[(NG + 7) / 8];
-  // ---- h1 = relu(W1 x + b1), h2 = relu(W2 h1 + b2)
-#pragma unroll
-  for (int layer = 0; layer < 2; ++layer) {
-#pragma unroll
-    for (int G = 0; G < NG; ++G) acc[G] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    if (layer == 0)
-      rt_kouter<NG, 1>(R, i, sb / 2, brow, acc PSEC_ARGS);
-    else
-      rt_kouter<NG, 2>(R, i, NG / 2, brow, acc PSEC_ARGS);
-    float* hg = (layer == 0 ? r.h1 : r.h2) + (long)myrow * H + 4 * g;
-    uint32_t (&m)[(NG + 7) / 8] = layer == 0 ? m1 : m2;
-#pragma unroll
-    for (int k = 0; k < (NG + 7) / 8; ++k) m[k] = 0;
-    f32x4 bias_all[NG];  // every bias fragment read before the row image is written
-#pragma unroll
-    for (int G = 0; G < NG; ++G) bias_all[G] = lds4(&lb[layer * H + 16 * G + 4 * g]);
-#pragma unroll
-    for (int G = 0; G < NG; ++G) {
-      const f32x4 bias = bias_all[G];
-      f32x4 v;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float x = acc[G][q] + bias[q];
-        v[q] = x > 0.0f ? x : 0.0f;
-        const uint32_t on = (__float_as_uint(v[q]) + 0x7fffffffu) >> 31;
-        m[G / 8] |= on << ((4 * G + q) % 32);
-      }
-      *reinterpret_cast<f32x4*>(arow + 16 * G) = v;  // in place: every read of the input is done
-      st_f4(hg + 16 * G, v);
-    }
-    PSEC(13);
-  }
-  // ---- [a1 | c1] = relu(h2 [Wa1; Wc1]^T + [ba1; bc1]), kept in registers
-  f32x4 av[NG], cv[NG];
-#pragma unroll
-  for (int G = 0; G < NG; ++G) av[G] = cv[G] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  for (int kb = 0; kb < NG; ++kb, ++i) {
-    R.advance(i);
-    const float* sl = R.slot(i);
-    const float* bp = brow + 16 * kb;
-    rt_piped<NG, 3>(
-        [&](int G, f32x4(&f)[3]) {
-          f[0] = lds4(sl + G * 256);
-          f[1] = lds4(sl + (NG + G) * 256);
-          f[2] = lds4(bp);
-        },
-        [&](int G, const f32x4(&f)[3]) { mfma4x2(f[0], f[1], f[2], f[2], av[G], cv[G]); });
-    PSEC(3);
-    __syncthreads();
-    PSEC(12);
-  }
-  // ---- loss head (ppo/agent.py:226-245), row c on every lane group
-  float p0 = 0.0f, p1 = 0.0f, pv = 0.0f;
-#pragma unroll
-  for (int G = 0; G < NG; ++G) {
-    const f32x4 ba = *reinterpret_cast<const f32x4*>(&lb[2 * H + 16 * G + 4 * g]);
-    const f32x4 bc = *reinterpret_cast<const f32x4*>(&lb[3 * H + 16 * G + 4 * g]);
-    const f32x4 w0 = *reinterpret_cast<const f32x4*>(&hw[16 * G + 4 * g]);
-    const f32x4 w1 = *reinterpret_cast<const f32x4*>(&hw[H + 16 * G + 4 * g]);
-    const f32x4 wcv = *reinterpret_cast<const f32x4*>(&hw[2 * H + 16 * G + 4 * g]);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float a = av[G][q] + ba[q], cc = cv[G][q] + bc[q];
-      a = a > 0.0f ? a : 0.0f;
-      cc = cc > 0.0f ? cc : 0.0f;
-      av[G][q] = a, cv[G][q] = cc;
-      p0 += a * w0[q];
-      p1 += a * w1[q];
-      pv += cc * wcv[q];
-    }
-  }
-  // the four lane groups' partials of row c, in group order
-  {
-    const float x0 = __shfl_xor(p0, 16), x1 = __shfl_xor(p1, 16), xv = __shfl_xor(pv, 16);
-    const bool lo = (g & 1) == 0;
-    p0 = lo ? p0 + x0 : x0 + p0;
-    p1 = lo ? p1 + x1 : x1 + p1;
-    pv = lo ? pv + xv : xv + pv;
-    const float y0 = __shfl_xor(p0, 32), y1 = __shfl_xor(p1, 32), yv = __shfl_xor(pv, 32);
-    const bool lo2 = g < 2;
-    p0 = lo2 ? p0 + y0 : y0 + p0;
-    p1 = lo2 ? p1 + y1 : y1 + p1;
-    pv = lo2 ? pv + yv : yv + pv;
-  }
-  float dmu0, dmu1, dv, tl[9];
-  {
-    // torch Normal: scale = exp(log_std); var = scale**2; log_scale = log(scale)
-    const float sc0 = expf(ls0), sc1 = expf(ls1);
-    const float var0 = sc0 * sc0, var1 = sc1 * sc1;
-    const float lsc0 = logf(sc0), lsc1 = logf(sc1);
-    const float LOG_SQRT_2PI = 0.91893853320467274178f;
-    const float invB = 1.0f / (float)r.B;
-    const float lo = 1.0f - r.eps_clip, hi = 1.0f + r.eps_clip;
-    const float mu0 = p0 + ba0, mu1 = p1 + ba1, val = pv + bcv;
-    const float d0 = hz0 - mu0, d1 = hz1 - mu1;
-    const float lp0 = -(d0 * d0) / (2.0f * var0) - lsc0 - LOG_SQRT_2PI;
-    const float lp1 = -(d1 * d1) / (2.0f * var1) - lsc1 - LOG_SQRT_2PI;
-    const float logp = (lp0 - hq0) + (lp1 - hq1);
-    const float log_ratio = logp - hold;
-    const float ratio = expf(log_ratio);
-    const float cr = fminf(fmaxf(ratio, lo), hi);
-    const float s1 = ratio * hadv, s2 = cr * hadv;
-    const float inr = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
-    // torch.min / clamp backward: ties split the gradient evenly
-    const float wsel = s1 < s2 ? 1.0f : (s1 > s2 ? inr : 0.5f * (1.0f + inr));
-    const float dlogp = -invB * hadv * wsel * ratio;  // d(actor_loss)/d(logp)
-    dmu0 = dlogp * d0 / var0;
-    dmu1 = dlogp * d1 / var1;
-    dv = r.value_coef * 2.0f * (val - hret) * invB;
-    tl[0] = dmu0, tl[1] = dmu1, tl[2] = dv;
-    tl[3] = dlogp * ((d0 * d0) / var0 - 1.0f);
-    tl[4] = dlogp * ((d1 * d1) / var1 - 1.0f);
-    tl[5] = -fminf(s1, s2);
-    tl[6] = (val - hret) * (val - hret);
-    tl[7] = fabsf(ratio - 1.0f) > r.eps_clip ? 1.0f : 0.0f;
-    tl[8] = (ratio - 1.0f) - log_ratio;
-  }
-  if (blockIdx.x == 0 && t == 0) {
-    r.counters[0] += 1;  // Adam step t for this minibatch
-    r.counters[1] += 1;  // metrics row (this step writes row counters[1]-1)
-  }
-  // head-parameter gradients of the wave's 16 rows (sums over the 16 lanes of each lane group)
-  // into the wave's row image (h2 is dead), then summed over the 4 waves in wave order
-  float* hp = act;  // [3H + 16] per wave
-#pragma unroll
-  for (int G = 0; G < NG; ++G) {
-    f32x4 s0, s1, sc;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      s0[q] = row16_sum(dmu0 * av[G][q]);
-      s1[q] = row16_sum(dmu1 * av[G][q]);
-      sc[q] = row16_sum(dv * cv[G][q]);
-    }
-    if (c == 0) {
-      *reinterpret_cast<f32x4*>(&hp[16 * G + 4 * g]) = s0;
-      *reinterpret_cast<f32x4*>(&hp[H + 16 * G + 4 * g]) = s1;
-      *reinterpret_cast<f32x4*>(&hp[2 * H + 16 * G + 4 * g]) = sc;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    const float v = row16_sum(tl[k]);
-    if (lane == 0) hp[3 * H + k] = v;
-  }
-  // dac = dL/d[a1 | c1] through the ReLUs (the reference's expression per element), in place
-  float* dacg = r.dac + (long)myrow * 2 * H + 4 * g;
-#pragma unroll
-  for (int G = 0; G < NG; ++G) {
-    const f32x4 w0 = *reinterpret_cast<const f32x4*>(&hw[16 * G + 4 * g]);
-    const f32x4 w1 = *reinterpret_cast<const f32x4*>(&hw[H + 16 * G + 4 * g]);
-    const f32x4 wcv = *reinterpret_cast<const f32x4*>(&hw[2 * H + 16 * G + 4 * g]);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {  // a1 / c1 are relu outputs: +0 or positive (bits != 0 <=> on)
-      av[G][q] = sel_on(av[G][q], dmu0 * w0[q] + dmu1 * w1[q]);
-      cv[G][q] = sel_on(cv[G][q], dv * wcv[q]);
-    }
-    st_f4(dacg + 16 * G, av[G]);
-    st_f4(dacg + H + 16 * G, cv[G]);
-  }
-  PSEC(7);
-  __syncthreads();
-  {
-    float* out = r.head_part + (long)blockIdx.x * r.HP;
-    const float* h0 = lds + L_RING;
-    for (int e = t; e < 3 * H + 9; e += 256)
-      out[e] = ((h0[e] + h0[16 * PW + e]) + h0[2 * 16 * PW + e]) + h0[3 * 16 * PW + e];
-  }
-  __syncthreads();  // the row images are written again below (dh2)
-  PSEC(4);
-  // ---- dh2 = (dac [Wa1; Wc1]) * (h2 > 0): 4 output blocks per group, B from the registers
-  float* dh2g = r.dh2 + (long)myrow * H + 4 * g;
-  for (int gg = 0; gg < NG / 4; ++gg) {
-    f32x4 d[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) d[u] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-    for (int ls = 0; ls < 4; ++ls, ++i) {
-      R.advance(i);
-      const float* sl = R.slot(i);
-      rt_piped<NG / 2, 4>(
-          [&](int kl, f32x4(&f)[4]) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) f[u] = lds4(sl + (4 * kl + u) * 256);
-          },
-          [&](int kl, const f32x4(&f)[4]) {
-            const int kb = (NG / 2) * ls + kl;  // k-block of K = 2H: < NG actor, else critic
-            const f32x4& b = kb < NG ? av[kb < NG ? kb : 0] : cv[kb >= NG ? kb - NG : 0];
-            mfma4x2(f[0], f[1], b, b, d[0], d[1]);
-            mfma4x2(f[2], f[3], b, b, d[2], d[3]);
-          });
-      PSEC(5);
-      __syncthreads();
-      PSEC(12);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int G = 4 * gg + u;
-      f32x4 v;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = sel_bit(m2[G / 8], (4 * G + q) % 32, d[u][q]);
-      *reinterpret_cast<f32x4*>(arow + 16 * G) = v;
-      st_f4(dh2g + 16 * G, v);
-    }
-    PSEC(13);
-  }
-  // ---- dh1 = (dh2 W2) * (h1 > 0)
-#pragma unroll
-  for (int G = 0; G < NG; ++G) acc[G] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  rt_kouter<NG, 6>(R, i, NG / 2, brow, acc PSEC_ARGS);
-  float* dh1g = r.dh1 + (long)myrow * H + 4 * g;
-#pragma unroll
-  for (int G = 0; G < NG; ++G) {
-    f32x4 v;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = sel_bit(m1[G / 8], (4 * G + q) % 32, acc[G][q]);
-    st_f4(dh1g + 16 * G, v);
-  }
-  PSEC(13);
-  PSEC_FLUSH;
 }
 
 // ----------------------------------------------------------------------------- acting
@@ -3080,14 +2598,7 @@ int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
     r.counters = a->counters;
     // 8 waves (2 per SIMD) when the columns split into 16-wide tiles, else 4
     const dim3 g1(w.n1), b4(256), b8(512), blk(256);
-    if (w.rows_t) {
-      switch (H / 64) {
-        case 1: hipLaunchKernelGGL((ppo_rowsT<1>), g1, b4, 0, s, r); break;
-        case 2: hipLaunchKernelGGL((ppo_rowsT<2>), g1, b4, 0, s, r); break;
-        case 3: hipLaunchKernelGGL((ppo_rowsT<3>), g1, b4, 0, s, r); break;
-        default: hipLaunchKernelGGL((ppo_rowsT<4>), g1, b4, 0, s, r); break;
-      }
-    } else if (w.rt == 2 * kRowTile) {
+    if (w.rt == 2 * kRowTile) {
       switch (H / 64) {
         case 1: hipLaunchKernelGGL((ppo_rows<1, 4, 32>), g1, b4, 0, s, r); break;
         case 2: hipLaunchKernelGGL((ppo_rows<2, 8, 32>), g1, b8, 0, s, r); break;

@@ -120,6 +120,56 @@ def flat_params(agent):
     return agent._flat
 
 
+# hidden width at which hwy_ppo_act runs ppo_act_c, the forward + head of the minibatch step's
+# compact row kernel, from a weight tile image (ppo_kernels.hip: hwy_ppo_act)
+_ACT_C_HIDDEN = 256
+
+
+class _TileImage:
+    """A weight tile image (hwy_ppo_sync_params) for acting when no FusedPPO keeps one in step
+    with the parameters: a fresh agent, or a checkpoint loaded before the first fused update.
+    At H = 256 acting then always runs ppo_act_c, whose bits are the minibatch step's, instead of
+    ppo_act on the params rows (equal only to fp32 rounding)."""
+
+    def __init__(self, agent, flat: torch.Tensor, S: int, H: int):
+        L = _bind(lib())
+        self.L, self.flat, self.S = L, flat, S
+        self.params = flat_params(agent)[3]
+        self.dims = PpoDims(64, S, H, 2)
+        ws = L.hwy_ppo_workspace_bytes(ctypes.byref(self.dims))
+        off = L.hwy_ppo_tile_image_offset(ctypes.byref(self.dims))
+        if ws < 0 or off < 0:
+            raise ValueError("unsupported fused PPO dims for a tile image")
+        self.workspace = torch.zeros(int(ws), device=flat.device, dtype=torch.uint8)
+        self.off = int(off)
+        self.version = None
+
+    def _versions(self):
+        return (self.flat._version,) + tuple(p._version for p in self.params)
+
+    def current(self) -> int:
+        if self.version != self._versions():
+            a = PpoArgs()
+            a.dims = self.dims
+            a.params, a.workspace = self.flat.data_ptr(), self.workspace.data_ptr()
+            check(self.L.hwy_ppo_sync_params(ctypes.byref(a), stream_ptr()), "hwy_ppo_sync_params")
+            self.version = self._versions()
+        return self.workspace.data_ptr() + self.off
+
+
+def _act_tiles(agent, flat: torch.Tensor, S: int, H: int) -> Optional[int]:
+    """A tile image in step with `flat`: the agent's FusedPPO's, rebuilt from the params when a
+    torch-side write retired it, else an acting-only one (_TileImage)."""
+    F = getattr(agent, "_fused", None)
+    if F is not None and F.flat is flat and F._tile_off is not None:
+        F.refresh_tiles()
+        return F.current_tiles(flat)
+    T = getattr(agent, "_act_tile_image", None)
+    if T is None or T.flat is not flat or T.S != S:
+        T = agent._act_tile_image = _TileImage(agent, flat, S, H)
+    return T.current()
+
+
 def act_supported(S: int, H: int, A: int) -> bool:
     return A == 2 and S % 4 == 0 and S <= 256 and H % 64 == 0 and 64 <= H <= 512
 
@@ -164,6 +214,8 @@ def fused_act(agent, states: torch.Tensor, deterministic: bool = False,
                                              value.data_ptr())
     F = getattr(agent, "_fused", None)
     a.tiles = F.current_tiles(flat) if F is not None else None
+    if a.tiles is None and H == _ACT_C_HIDDEN:
+        a.tiles = _act_tiles(agent, flat, S, H)
     check(_bind(lib()).hwy_ppo_act(ctypes.byref(a), stream_ptr()), "hwy_ppo_act")
     return action, pre, logp, value
 
@@ -233,13 +285,23 @@ class FusedPPO:
         t = int(self.counters[0].item())
         if t == 0:
             return
-        for p, off in zip(self.params, self.offs):
-            n = p.numel()
-            opt.state[p] = {
-                "step": torch.tensor(float(t), device=p.device if opt.defaults.get("capturable") else "cpu"),
-                "exp_avg": self.m[off:off + n].view_as(p).clone(),
-                "exp_avg_sq": self.v[off:off + n].view_as(p).clone(),
-            }
+        with torch.no_grad():
+            for p, off in zip(self.params, self.offs):
+                n = p.numel()
+                m, v = self.m[off:off + n].view_as(p), self.v[off:off + n].view_as(p)
+                st = opt.state.get(p)
+                if st and all(k in st for k in ("step", "exp_avg", "exp_avg_sq")) and \
+                        st["exp_avg"].shape == p.shape:
+                    # in place: a captured torch learner's graph still points at these tensors
+                    st["exp_avg"].copy_(m)
+                    st["exp_avg_sq"].copy_(v)
+                    st["step"].fill_(float(t))
+                    continue
+                opt.state[p] = {
+                    "step": torch.tensor(float(t), device=p.device if opt.defaults.get("capturable") else "cpu"),
+                    "exp_avg": m.clone(),
+                    "exp_avg_sq": v.clone(),
+                }
 
     # -------------------------------------------------------------- steps
     def _args(self, states, pre_tanh, old_lp, adv, ret, idx_ptr: int) -> PpoArgs:
@@ -277,6 +339,16 @@ class FusedPPO:
         needed before a step whenever params changed outside hwy_ppo_optimizer."""
         check(self.L.hwy_ppo_sync_params(ctypes.byref(a), stream_ptr()), "hwy_ppo_sync_params")
 
+    def refresh_tiles(self):
+        """Rebuild the tile image from the flat params if a torch-side write retired it."""
+        if self._tile_off is None or self._tiles_version == self._param_versions():
+            return
+        a = PpoArgs()
+        a.dims = self.dims
+        a.params, a.workspace = self.flat.data_ptr(), self.workspace.data_ptr()
+        self.sync_params(a)
+        self._tiles_version = self._param_versions()
+
     def current_tiles(self, flat: torch.Tensor) -> Optional[int]:
         """Device address of the weight tile image when it is in step with `flat` (it is after
         run(): hwy_ppo_optimizer rewrites it with the weights; any torch-side write to the
@@ -310,12 +382,10 @@ class FusedPPO:
         # an instance not (yet) registered as agent._fused takes the state over the same way
         ag = self.agent
         if hasattr(ag, "_adam_to") and getattr(ag, "_fused", None) in (None, self):
-            if ag._fused is self:
-                ag._adam_to("fused")
-            else:
-                if ag._adam_owner != "fused":
-                    self._import_torch_state()
-                ag._adam_owner = "fused"
+            # an unregistered instance registers as it takes the Adam state over, so the agent
+            # can export it back (save(), a torch-path update) instead of using stale state
+            ag._fused = self
+            ag._adam_to("fused")
         # the captured graphs bake in the buffer addresses and the scalar hyper-parameters of
         # PpoArgs: a change to either (an lr schedule, agent.eps_clip, ...) forces a recapture
         key = (states.data_ptr(), pre_tanh.data_ptr(), old_lp.data_ptr(), adv.data_ptr(),

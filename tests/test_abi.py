@@ -110,3 +110,13 @@ def test_product_library_reads_no_development_knobs(lib):
     # every getenv of the PPO kernels sits inside the HWY_DEV_KNOBS block
     dev = src[src.index("#ifdef HWY_DEV_KNOBS"):src.index("#endif", src.index("#ifdef HWY_DEV_KNOBS"))]
     assert src.count("getenv(") == dev.count("getenv(")
+
+
+def test_product_library_holds_only_reachable_row_kernels():
+    """Kernels no product launch selects are not built into libhwy.so (the
+    transposed ppo_rowsT row kernel was compiled in but reachable only through a dev knob)."""
+    blob = open(LIB_PATH, "rb").read()
+    assert b"ppo_rowsT" not in blob
+    for name in (b"ppo_rows_c", b"ppo_wgrad", b"ppo_wsum", b"ppo_adam", b"ppo_act_c",
+                 b"hwy_step_kernel"):
+        assert name in blob, name

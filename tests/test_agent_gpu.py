@@ -86,7 +86,15 @@ def test_training_routine_vectorised(tmp_path, monkeypatch):
     env.close()
 
 
-def test_training_routine_single_env_reference_loop(tmp_path, monkeypatch):
+def test_configs0_single_env_reference_loop(tmp_path, monkeypatch, caplog):
+    """BASELINE configs[0]: the reference's own one-env loop (training/routine.py:121-243) at the
+    config-1 hyperparameters (experiments/config.py:33-37 with hidden_dim 64: lr 1e-4, 6 epochs,
+    batch_size 64, 2048 steps per update), sorted observation, no PE.  It runs until at least one
+    full 2048-sample update has completed; the update's metrics must be finite and logged in the
+    reference's update_complete format (ppo/agent.py:289-298)."""
+    import logging
+    import re
+
     from config.base_config import HIGHWAY_CONFIG
     from experiments.config import Condition
     from experiments.wrappers import make_env
@@ -94,10 +102,26 @@ def test_training_routine_single_env_reference_loop(tmp_path, monkeypatch):
     from training.routine import train_with_experiment_name
 
     monkeypatch.chdir(tmp_path)
+    caplog.set_level(logging.INFO)
     env = make_env(Condition.SORTED, HIGHWAY_CONFIG)
-    agent = PPOAgent(60, 2, epochs=1, hidden_dim=32, device=torch.device("cuda", 0), use_graphs=False)
-    rewards, avg, mh = train_with_experiment_name(env, agent, max_episodes=4, target_reward=1e9,
-                                                  eval_interval=2, steps_per_update=64,
-                                                  experiment_name="t_one", exp_seed=42)
-    assert len(rewards) == 3 and mh["episode_numbers"][:4] == [1, 2, 3, 4]
+    assert env.observation_space.shape == (15, 4)
+    torch.manual_seed(42)
+    agent = PPOAgent(60, 2, lr=1e-4, epochs=6, batch_size=64, hidden_dim=64,
+                     device=torch.device("cuda", 0))
+    rewards, avg, mh = train_with_experiment_name(env, agent, max_episodes=150, target_reward=1e9,
+                                                  eval_interval=1000, steps_per_update=2048,
+                                                  experiment_name="configs0", exp_seed=42)
     env.close()
+    ups = mh["policy_updates"]
+    assert any(u["steps"] >= 2048 for u in ups), "no 2048-sample update in 150 episodes"
+    keys = ["loss", "policy_loss", "value_loss", "entropy", "clip_fraction", "approx_kl",
+            "explained_variance"]
+    for u in ups:
+        for k in keys:
+            assert np.isfinite(u[k]), (k, u)
+    fmt = re.compile(r"^update_complete loss=-?\d+\.\d{4} policy_loss=-?\d+\.\d{4} "
+                     r"value_loss=-?\d+\.\d{4} entropy=-?\d+\.\d{4} clip_frac=-?\d+\.\d{3} "
+                     r"kl=-?\d+\.\d{5} explained_var=-?\d+\.\d{3}$")
+    lines = [r.getMessage() for r in caplog.records if r.getMessage().startswith("update_complete")]
+    assert len(lines) == len(ups) and all(fmt.match(l) for l in lines), lines[:2]
+    assert (tmp_path / "artifacts/highway-ppo/summary_configs0.csv").exists()

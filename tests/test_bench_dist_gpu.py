@@ -36,3 +36,12 @@ def test_bench_two_ranks_one_line():
     assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["cpu_baseline"] is None
     assert d["config"]["global_envs"] == 512 and d["roofline"]["includes_allreduce"] is True
     assert abs(d["value"] - 512 * 8 * 2 / (d["ms_per_step"] * 2e-3)) / d["value"] < 0.01
+    # the all-reduce's own cost beside the step it burdens: the flat gradient
+    # bucket of ActorCritic(60, 2, 256) in fp32, timed alone, and the step time that includes it
+    roof = d["roofline"]
+    S, H = 60, 256
+    n_params = S * H + H + 3 * (H * H + H) + 2 * H + 2 + 2 + H + 1
+    ar = roof["allreduce"]
+    assert ar["bytes"] == 4 * n_params and ar["us_per_allreduce"] > 0
+    assert roof["step_us_with_allreduce"] == roof["avg_launch_us"] > 0
+    assert 0 < roof["allreduce_share_of_step"] == round(ar["us_per_allreduce"] / roof["avg_launch_us"], 4)

@@ -188,8 +188,8 @@ def _check_grads(ga, gb, g64, msg=""):
                                     # slices; H 512: 104 tiles x 2 slices)
                                     (120, 256, 32768), (120, 384, 32768), (120, 512, 32768),
                                     (240, 256, 32768), (240, 384, 32768), (240, 512, 32768),
-                                    # ppo_rowsT (64-row workgroups, >= 64 rows per CU) at the
-                                    # narrower learners: 4, 8 and 12 output blocks per layer
+                                    # 32-row ppo_rows workgroups (4 or 8 waves) at the narrower
+                                    # learners, H 64 / 128 / 192, with the balanced wgrad split
                                     (60, 64, 16384), (60, 128, 16384), (136, 192, 16384)])
 def test_fused_gradient_matches_autograd(S, H, mb):
     """One fused forward/backward against autograd on the same minibatch.  The reference
@@ -482,38 +482,47 @@ def test_fused_act_matches_actor_critic_act(S, H, B):
 @pytest.mark.parametrize("S,H", [(60, 256), (120, 192)])
 def test_fused_act_from_tile_image_equals_params_path(S, H):
     """After a fused update the acting kernel streams the update's weight tile image
-    (hwy_ppo_tile_image_offset); results are bit-identical to reading the flat params (at
-    H = 256 the image path is the compact kernel and agrees to fp32 rounding), and a torch-side
-    parameter write (load_state_dict) retires the image until the next update."""
+    (hwy_ppo_tile_image_offset).  A torch-side parameter write (load_state_dict) retires the
+    image; acting then rebuilds it from the params (hwy_ppo_sync_params), so the same weights act
+    to the same bits on either side of a checkpoint reload -- at H = 256 always through
+    ppo_act_c, whose head is the minibatch step's -- and a fresh agent holding those
+    weights acts to the same bits too."""
     from hwy.ppo_native import fused_act
 
     a, b = _agents(S, H)
     n, nmb = 1024, 4
     s, z, lp, adv, ret, perm = _data(n, S, a)
     F = FusedPPO(b, n // nmb, nmb, use_graphs=False)
-    b._fused = F
     F.run(s, z, lp, adv.clone(), ret.clone(), perm.clone())
+    assert b._fused is F  # run() registers the instance that took the Adam state over
     flat = F.flat
     assert F.current_tiles(flat) is not None
     x = torch.randn(777, S, device=DEV)
     with torch.no_grad():
         got_t = fused_act(b, x, generator=torch.Generator(device=DEV).manual_seed(5))
-        saved = F._tiles_version
-        F._tiles_version = None  # force the params path
+        F._tiles_version = None  # retired image: rebuilt from the params on the next act
         got_p = fused_act(b, x, generator=torch.Generator(device=DEV).manual_seed(5))
-        F._tiles_version = saved
+    assert F.current_tiles(flat) is not None
     for t_, p_ in zip(got_t, got_p):
-        if H == 256:  # ppo_act_c (register head) against ppo_act: fp32 agreement
-            torch.testing.assert_close(t_, p_, rtol=1e-4, atol=2e-5)
-        else:  # the same kernel on both paths: bit-identical
-            assert torch.equal(t_, p_)
-    # a torch-side write bumps the flat buffer's version: acting falls back to params
-    b.actor_critic.load_state_dict(a.actor_critic.state_dict())
+        assert torch.equal(t_, p_)
+    # checkpoint round trip: load_state_dict retires the image, acting is bit-identical after it
+    sd = {k: v.clone() for k, v in b.actor_critic.state_dict().items()}
+    b.actor_critic.load_state_dict(sd)
     assert F.current_tiles(flat) is None
     with torch.no_grad():
-        ref = a.actor_critic.act(x, deterministic=True)
-        got = fused_act(b, x, deterministic=True)
-    for r, g in zip(ref, got):
+        got_l = fused_act(b, x, generator=torch.Generator(device=DEV).manual_seed(5))
+    for t_, l_ in zip(got_t, got_l):
+        assert torch.equal(t_, l_)
+    # a fresh agent (no FusedPPO yet) with the same weights: same kernel, same bits
+    c, _ = _agents(S, H)
+    c.actor_critic.load_state_dict(sd)
+    with torch.no_grad():
+        got_c = fused_act(c, x, generator=torch.Generator(device=DEV).manual_seed(5))
+        ref = c.actor_critic.act(x, deterministic=True)
+        det = fused_act(c, x, deterministic=True)
+    for t_, c_ in zip(got_t, got_c):
+        assert torch.equal(t_, c_)
+    for r, g in zip(ref, det):
         torch.testing.assert_close(g, r, rtol=1e-4, atol=2e-5)
 
 

@@ -67,6 +67,11 @@ def main():
     p.add_argument("--lr", type=float, default=3e-4)
     p.add_argument("--epochs", type=int, default=8)
     p.add_argument("--hidden", type=int, default=256)
+    p.add_argument("--obs-vehicles", type=int, default=0,
+                   help="observation vehicles_count (0: HIGHWAY_CONFIG's 15); bench configs[2]/[4]: 30")
+    p.add_argument("--order", choices=["sorted", "shuffled"], default=None,
+                   help="observation order set explicitly, as bench.py does (default: make_env's own)")
+    p.add_argument("--d-embed", type=int, default=4, help="PE d_embed / rotate_dim")
     args = p.parse_args()
 
     out = os.path.abspath(args.out)
@@ -81,11 +86,18 @@ def main():
     cond = {"sorted": Condition.SORTED, "shuffled_rope": Condition.SHUFFLED_ROPE,
             "shuffled_distpe": Condition.SHUFFLED_DISTPE,
             "shuffled_rankpe": Condition.SHUFFLED_RANKPE}[args.condition]
-    d_embed = None if args.condition == "sorted" else 4
+    d_embed = None if args.condition == "sorted" else args.d_embed
+    obs_over = {}
+    if args.obs_vehicles:
+        obs_over["vehicles_count"] = args.obs_vehicles
+    if args.order:
+        obs_over["order"] = args.order
     for seed in args.seeds:
         name = (f"{args.condition}_lr{args.lr:g}_hidden_dim{args.hidden}_clip_eps0.2_"
                 f"entropy_coef0.005_epochs{args.epochs}_batch_size64"
                 + (f"_d_embed{d_embed}" if d_embed else "")
+                + (f"_obs{args.obs_vehicles}" if args.obs_vehicles else "")
+                + (f"_{args.order}" if args.order else "")
                 + f"_seed{seed}" + (f"_envs{args.num_envs}" if args.num_envs > 1 else "")
                 + (f"_T{args.rollout}_mb{args.minibatches}" if args.rollout else ""))
         hp = ConditionHP(lr=args.lr, clip_eps=0.2, epochs=args.epochs, batch_size=64,
@@ -99,7 +111,8 @@ def main():
         if args.minibatches:
             extra["num_minibatches"] = args.minibatches
         exp = Experiment(name=name, condition=cond, hp=hp, seed=seed,
-                         max_episodes=args.episodes, target_reward=130.0, extra=extra)
+                         max_episodes=args.episodes, target_reward=130.0, extra=extra,
+                         env_config_overrides={"observation": obs_over} if obs_over else {})
         run_dir = os.path.join(out, f"{args.condition}_seed{seed}")
         os.makedirs(run_dir, exist_ok=True)
         cwd = os.getcwd()
@@ -114,6 +127,8 @@ def main():
                "num_envs": args.num_envs, "episodes": args.episodes, "rollout": args.rollout,
                "minibatches": args.minibatches, "eval_interval": args.eval_interval,
                "lr": args.lr, "epochs": args.epochs, "hidden_dim": args.hidden,
+               "obs_vehicles": args.obs_vehicles or 15, "order": args.order or "make_env default",
+               "d_embed": d_embed,
                "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else "cpu"}
         if res["status"] == "COMPLETED":
             avg = res["avg_rewards"]
