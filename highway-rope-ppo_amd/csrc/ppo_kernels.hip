@@ -118,6 +118,12 @@ constexpr int kMaxRowS = 256;  // states dim bound of the fused path (LDS)
 #ifndef HWY_WG_DMA
 #define HWY_WG_DMA 1  // ppo_wgrad stages its chunks by LDS-DMA (wgrad_tile_dma); 0: register staging
 #endif
+#ifndef HWY_WG_SPREAD
+#define HWY_WG_SPREAD 0  // 1: ppo_wgrad's LDS-DMA pieces issued between the MFMA groups
+#endif
+#ifndef HWY_RING_RA
+#define HWY_RING_RA 0  // 1: the row kernels' activation reads pinned one block ahead
+#endif
 #ifndef HWY_RING_DC
 #define HWY_RING_DC 2  // weight blocks in flight per wave in the compact-LDS ppo_rows
 #endif
@@ -931,6 +937,11 @@ struct WRing {
           a[rb] = a_nxt[rb];
           a_nxt[rb] = *reinterpret_cast<const f32x4*>(arow + 16 * rb * pa + kn);
         }
+#if HWY_RING_RA
+        // pinned: the next block's activation reads go out before this block's MFMAs (the
+        // scheduler otherwise sinks them to the block's end, right before their use)
+        __builtin_amdgcn_sched_barrier(0);
+#endif
         const bool kin = kb + 4 * g < sg[SEG].K;  // else the block was clamped: weights are 0
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -1825,16 +1836,19 @@ typedef __attribute__((address_space(3))) void lds_void_t;
   const int rb = lane >> 4, qb = lane & 15;
   const uint32_t a_col = (uint32_t)min(i0 + 4 * (h ? ((l32 - 8) & 31) : l32), M - 4);
   const uint32_t b_col = (uint32_t)min(j0 + 4 * ((rb & 1) ? ((qb - 8) & 15) : qb), N - 4);
-  auto dma = [&](int c, float* buf) {
+  // part 0: A pieces 0-1, part 1: A pieces 2-3, part 2: the two B pieces; -1: all three
+  auto dma = [&](int c, float* buf, int part = -1) {
     const int k0 = kb0 + 64 * c;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+      if (part >= 0 && part != i / 2) continue;
       const uint32_t row = (uint32_t)min(k0 + 2 * (4 * w + i) + h, kb1 - 1);
       __builtin_amdgcn_global_load_lds((const void*)(A + (row * (uint32_t)lda + a_col)),
                                        (lds_void_t*)(buf + (4 * w + i) * 256), 16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < (HWY_WG_EXP == 5 ? 0 : 2); ++i) {
+      if (part >= 0 && part != 2) continue;
       const uint32_t row = (uint32_t)min(k0 + 4 * (2 * w + i) + rb, kb1 - 1);
       __builtin_amdgcn_global_load_lds((const void*)(Bm + (row * (uint32_t)ldb + b_col)),
                                        (lds_void_t*)(buf + kWgTM * 64 + (2 * w + i) * 256), 16,
@@ -1853,7 +1867,9 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 #pragma unroll
   for (int q = 0; q < 16; ++q) acc0[q] = acc1[q] = 0.0f;
   float bs0 = 0.0f, bs1 = 0.0f;  // A column sums of this lane's features over its rows
-  auto compute = [&](const float* buf, int lim, auto mask_tag) {
+  // dc / dbuf: the chunk whose DMAs go out between this chunk's MFMA groups (HWY_WG_SPREAD;
+  // dc < 0: none)
+  auto compute = [&](const float* buf, int lim, auto mask_tag, int dc, float* dbuf) {
     constexpr bool MASK = decltype(mask_tag)::value;  // rows >= lim (of the chunk) are zero
     const float* pa0 = buf + offa0 + 32 * kh * 128;
     const float* pa1 = buf + offa1 + 32 * kh * 128;
@@ -1890,6 +1906,10 @@ typedef __attribute__((address_space(3))) void lds_void_t;
         acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(u1, y[b][j], acc1, 0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
+      if (HWY_WG_SPREAD && g < 3 && dc >= 0) {
+        dma(dc, dbuf, g);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
   };
   const std::integral_constant<bool, true> masked;
@@ -1912,8 +1932,9 @@ typedef __attribute__((address_space(3))) void lds_void_t;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (c + 2 < nchunk) dma(c + 2, b2);  // into chunk c - 1's buffer
-    compute(b0, kb1 - (kb0 + 64 * c), mask_tag);
+    // chunk c + 2 into chunk c - 1's buffer: here, or spread between this chunk's MFMA groups
+    if (!HWY_WG_SPREAD && c + 2 < nchunk) dma(c + 2, b2);
+    compute(b0, kb1 - (kb0 + 64 * c), mask_tag, c + 2 < nchunk ? c + 2 : -1, b2);
     float* tb = b0;
     b0 = b1, b1 = b2, b2 = tb;
   };

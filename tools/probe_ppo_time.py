@@ -36,3 +36,8 @@ for _ in range(reps):
 ev1.record()
 torch.cuda.synchronize()
 print(f"H={H}: {ev0.elapsed_time(ev1) / (reps * nmb) * 1e3:.1f} us per minibatch step", flush=True)
+# bit-identity fingerprint of the final weights (variants that only reorder instructions must
+# print the same value as the product library)
+import hashlib
+
+print(f"weights sha1 {hashlib.sha1(F.flat.detach().cpu().numpy().tobytes()).hexdigest()[:16]}", flush=True)

@@ -19,6 +19,6 @@ timeout -k 10 ${RUN_LIMIT:-1000} python -u tools/train_parity.py --seeds $SEEDS 
 rc=$?
 find "$OUT" -name '*.pth' -delete
 find "$OUT" -type d -name artifacts -prune -exec rm -rf {} +
-[ -s "$OUT/summary.jsonl" ] && python tools/recipe_stats.py "$OUT" "$COND h$HID E=$E T=$T $EPISODES episodes" > "$OUT/stats.json"
+[ -s "$OUT/summary.jsonl" ] && python tools/recipe_stats.py "$OUT" --note "$COND h$HID E=$E T=$T $EPISODES episodes $EXTRA" > "$OUT/stats.json"
 grep -h '"mean\|matched' "$OUT/stats.json" 2>/dev/null | head -8
 exit $rc
