@@ -174,6 +174,14 @@ __device__ unsigned long long g_hwy_wave_t[5 * HWY_NWT];
 #define WAVE_HWID() 0ull
 #endif
 
+// Development pricing builds only (make variant VEXTRA=-DHWY_SKIP=mask; WRONG results, never the
+// product): skip one part of the frame to price its instruction count (tools/ab.sh MODE=pmc).
+// 1 MOBIL, 2 the SAT pair loop, 4 collision candidates + SAT, 8 the abort loop, 16 steering,
+// 32 the IDM pow, 64 the observation's rank count
+#ifndef HWY_SKIP
+#define HWY_SKIP 0
+#endif
+
 // ------------------------------------------------------------------------- vehicle state
 struct Veh {
   float x, y, h, spd, tsp, dlt, tmr, ix, iy;
@@ -218,6 +226,7 @@ __device__ __forceinline__ float desired_gap(float a_spd, float a_c, float a_s, 
 __device__ __forceinline__ float idm_free(float ev_spd, float ev_tsp, float delta, float limit) {
   float tsp = hm_clipf(ev_tsp, 0.0f, limit);
   float base = hm_maxf(ev_spd, 0.0f) / hm_absf(hm_not_zero(tsp));
+  if (HWY_SKIP & 32) return hm_fma(-COMFORT_ACC_MAX, base * base, COMFORT_ACC_MAX);
   return hm_fma(-COMFORT_ACC_MAX, hm_powf(base, delta), COMFORT_ACC_MAX);
 }
 
@@ -481,7 +490,9 @@ __device__ void observe_wave(const hwy_config& C, int lane, const Veh& v, float 
               (C.see_behind || -2.0f * VEH_LENGTH < v.x - ex);
   const uint64_t em = ballot(elig);
   int rank;
-  if (C.order == HWY_ORDER_SORTED) {
+  if (C.order == HWY_ORDER_SORTED && (HWY_SKIP & 64)) {
+    rank = __popcll(em & ((1ull << lane) - 1ull));
+  } else if (C.order == HWY_ORDER_SORTED) {
     float key = hm_absf(v.x - ex);
     rank = 0;
     // four vehicles per round: their keys are read first, then compared (no branch per vehicle)
@@ -867,7 +878,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   SEC(sp, 2);
   int ntl = v.tl;
   bool gain[2] = {false, false};
-  if (fire) {
+  if (fire && !(HWY_SKIP & 1)) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int c = v.ln - 1 + 2 * q;
@@ -883,26 +894,30 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
     }
   }
   if (wave_any(gain[0] || gain[1])) {
-    float nf_x[2], nf_spd[2], nf_c[2], nf_s[2], nf_tsp[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {  // all lanes active: ds_bpermute
-      const int b = ri[2 * q] >= 0 ? ri[2 * q] : lane;
-      nf_x[q] = shf(v.x, b);
-      nf_spd[q] = shf(v.spd, b);
-      nf_c[q] = shf(ch, b);
-      nf_s[q] = shf(sh, b);
+    // upstream tries left, then right, and a passing right side overrides the left: so each
+    // lane first evaluates the side that decides if it passes -- the right where it gains, else
+    // the left -- in one pass over the lanes (one new-follower IDM, a pow, instead of two), and
+    // only lanes whose right side gained but failed the braking test evaluate their left side
+    // after it (rare).  The same arithmetic per side as the sequential order, so the same bits.
+    auto new_follower_ok = [&](int q) {
+      const int rq = q ? ri[2] : ri[0];
+      const int b = rq >= 0 ? rq : lane;  // all lanes active: ds_bpermute
+      const float nf_x = shf(v.x, b), nf_spd = shf(v.spd, b), nf_c = shf(ch, b), nf_s = shf(sh, b);
       const float tsp_b = shf(v.tsp, b);
-      nf_tsp[q] = (b == 0) ? 0.0f : tsp_b;  // plain Vehicle (ego) has no target_speed
-    }
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {  // left, then right (the right one overrides)
-      if (!gain[q]) continue;
+      const float nf_tsp = (b == 0) ? 0.0f : tsp_b;  // plain Vehicle (ego) has no target_speed
       float nfp = 0.0f;
-      if (ri[2 * q] >= 0)
-        nfp = idm_acc(nf_spd[q], nf_tsp[q], nf_x[q], nf_c[q], nf_s[q], true, v.x, v.spd, ch, sh,
-                      v.dlt, limit);
-      if (nfp < -LANE_CHANGE_MAX_BRAKING_IMPOSED) continue;
-      ntl = v.ln - 1 + 2 * q;
+      if (rq >= 0)
+        nfp = idm_acc(nf_spd, nf_tsp, nf_x, nf_c, nf_s, true, v.x, v.spd, ch, sh, v.dlt, limit);
+      return !(nfp < -LANE_CHANGE_MAX_BRAKING_IMPOSED);
+    };
+    const int q1 = gain[1] ? 1 : 0;
+    const bool nok = new_follower_ok(q1);  // every lane (the gathers need all 64 active)
+    const bool ok1 = (gain[0] || gain[1]) && nok;
+    if (ok1) ntl = v.ln - 1 + 2 * q1;
+    const bool retry = gain[1] && !ok1 && gain[0];
+    if (wave_any(retry)) {
+      const bool ok0 = new_follower_ok(0);
+      if (retry && ok0) ntl = v.ln - 1;
     }
   }
 
@@ -910,17 +925,24 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   // abort an ongoing lane change if another car targets the same lane within its desired gap,
   // in road order (lower indices already final, higher ones at their frame-start target)
   int tl_cur = ntl;
-  uint64_t cm = ballot(actor && mid);
+  uint64_t cm = (HWY_SKIP & 8) ? 0ull : ballot(actor && mid);
+  // a lane can trigger an abort only while its visible target is not its own lane (vis == tj
+  // and ln != tj), under either visibility; aborts only ever clear that, so this superset holds
+  // for the whole loop
+  const bool can = v.present && lane != 0 && (tl_cur != v.ln || tl_old != v.ln);
   while (cm) {
     const int j = __builtin_ctzll(cm);
     cm &= cm - 1ull;
     const int tj = rdli(tl_cur, j);
-    const float xj = rdlf(v.x, j), vj = rdlf(v.spd, j), cj = rdlf(ch, j), sj = rdlf(sh, j);
     const int vis = (lane < j) ? tl_cur : tl_old;
+    // the target-lane part of upstream's test first: most vehicles find no other car targeting
+    // their lane, and then the gap test (four broadcasts and a desired_gap) is skipped
+    const bool cheap = can && lane != j && v.ln != tj && vis == tj;
+    if (!wave_any(cheap)) continue;
+    const float xj = rdlf(v.x, j), vj = rdlf(v.spd, j), cj = rdlf(ch, j), sj = rdlf(sh, j);
     const float d = v.x - xj;
     const float d_star = desired_gap(vj, cj, sj, v.spd, ch, sh);
-    const bool cond = v.present && lane != j && lane != 0 && v.ln != tj && vis == tj &&
-                      (0.0f < d) && (d < d_star);
+    const bool cond = cheap && (0.0f < d) && (d < d_star);
     if (wave_any(cond) && lane == j) tl_cur = v.ln;
   }
   v.tl = tl_cur;
@@ -940,7 +962,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   const float ft_x = shf(v.x, st_), ft_spd = shf(v.spd, st_), ft_c = shf(ch, st_),
               ft_s = shf(sh, st_);
   if (actor) {
-    const float steer = steering_tan(v.y, v.h, v.spd, v.tl);
+    const float steer = (HWY_SKIP & 16) ? 0.0f : steering_tan(v.y, v.h, v.spd, v.tl);
     float acc = self_a;
     if (need_t) {
       const float acc_t =
@@ -1015,6 +1037,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
     const float xs = shf(v.x, ro.ord);  // x at position `lane`
     float xu = xs;
     bool up = lane < npres;
+    if (HWY_SKIP & 4) up = false;
     for (int o = 1; wave_any(up); ++o) {
       xu = __int_as_float(shl1i(__float_as_int(xu)));  // x at position lane + o
       up = up && lane + o < npres && !(hm_absf(xu - xs) > xbound);
@@ -1044,7 +1067,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
     cl.plist[off++] = (uint16_t)((lo << 8) | hi);
   }
   wave_lds_sync();
-  for (int base = 0; base < total; base += WAVE) {
+  for (int base = 0; base < ((HWY_SKIP & 2) ? 0 : total); base += WAVE) {
     const bool has = base + lane < total;
     const int pr = has ? cl.plist[base + lane] : 0;
     const int a = pr >> 8, b = pr & 0xff;  // a < b

@@ -1,0 +1,157 @@
+// Micro-benchmark (development aid): sustained rate of v_mfma_f32_16x16x4_f32 on MI355X for the
+// ppo_rows inner-loop shape -- per wave RB x TW = 2 x 2 accumulators, 16 MFMAs per 16-deep block
+// -- at 1, 2 and 4 waves per SIMD, with operands (a) in registers, (b) A from LDS (ds_read_b128
+// one block ahead) and B from a global ring (global_load_dwordx4, 2 blocks ahead) as ppo_rows_c
+// streams them.  Prints TFLOP/s and the fraction of the 157.3 TF/s fp32 MFMA peak.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int MODE>
+__global__ void __launch_bounds__(512) mfma_loop(const float* __restrict__ w, float* out, int nblk) {
+  __shared__ __attribute__((aligned(16))) float act[32 * 264];
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  for (int i = threadIdx.x; i < 32 * 264; i += blockDim.x) act[i] = 0.001f * (i % 97);
+  __syncthreads();
+  f32x4 acc[2][2] = {};
+  f32x4 a_nxt[2], buf[2][2];
+  const float* arow = act + c * 264 + 4 * g;
+  const f32x4* wp = reinterpret_cast<const f32x4*>(w) + (threadIdx.x >> 6) * 64 * 2 + lane;
+  for (int rb = 0; rb < 2; ++rb)
+    a_nxt[rb] = (MODE & 1) ? *reinterpret_cast<const f32x4*>(arow + 16 * rb * 264)
+                           : f32x4{1.0f, 2.0f, 3.0f, 4.0f} * (float)(lane + rb);
+  for (int d = 0; d < 2; ++d)
+    for (int t = 0; t < 2; ++t)
+      buf[d][t] = (MODE & 2) ? wp[(d * 2 + t) * 64 * 8] : f32x4{0.5f, 0.25f, 0.125f, 1.0f} * (float)(t + d);
+  for (int b0 = 0; b0 < nblk; b0 += 2) {
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      f32x4 a[2];
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        a[rb] = a_nxt[rb];
+        if (MODE & 1)
+          a_nxt[rb] = *reinterpret_cast<const f32x4*>(arow + 16 * rb * 264 + (((b0 + d + 1) & 15) * 16));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb)
+            acc[rb][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rb][j], buf[d][t][j], acc[rb][t], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (MODE & 2) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) buf[d][t] = wp[(((b0 + d + 2) & 63) * 2 + t) * 64 * 8];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  float s = 0.0f;
+  for (int rb = 0; rb < 2; ++rb)
+    for (int t = 0; t < 2; ++t) s += acc[rb][t][0] + acc[rb][t][1] + acc[rb][t][2] + acc[rb][t][3];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+// the ppo_wgrad chunk loop's shape: v_mfma_f32_32x32x2_f32, two accumulators per wave sharing
+// the B operand, operands read from LDS per k-step (one float per lane per operand)
+__global__ void __launch_bounds__(512) wg_loop(float* out, int nchunk) {
+  __shared__ float lds[64 * 192];
+  const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+  for (int i = threadIdx.x; i < 64 * 192; i += blockDim.x) lds[i] = 0.001f * (i % 89);
+  __syncthreads();
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  f32x16 acc0 = {}, acc1 = {};
+  for (int c = 0; c < nchunk; ++c) {
+    const float* buf = lds + (c & 1) * 0;
+    const float* pa0 = buf + h * 128 + l32;
+    const float* pa1 = pa0 + 32 * (1 + 0);
+    const float* pb = buf + 128 * 64 + h * 64 + l32;
+    float x0[2][4], x1[2][4], y[2][4];
+    auto rd = [&](int g, int b) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int st = 4 * g + j;
+        x0[b][j] = pa0[st * 256];
+        x1[b][j] = pa1[st * 256];
+        y[b][j] = pb[st * 128];
+      }
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int b = g & 1;
+      if (g + 1 < 4) rd(g + 1, b ^ 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(x0[b][j], y[b][j], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(x1[b][j], y[b][j], acc1, 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  float s = 0.0f;
+  for (int q = 0; q < 16; ++q) s += acc0[q] + acc1[q];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+int main() {
+  int cus = 0;
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+  std::vector<float> hw(64 * 2 * 64 * 8 * 64 * 4, 0.01f);
+  float *w, *out;
+  hipMalloc(&w, hw.size() * 4);
+  hipMemcpy(w, hw.data(), hw.size() * 4, hipMemcpyHostToDevice);
+  hipMalloc(&out, (size_t)cus * 4 * 512 * 4);
+  const int nblk = 4096;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  for (int mode = 0; mode < 4; ++mode)
+    for (int wps : {1, 2, 4}) {  // waves per SIMD: workgroups of 4 waves x wps per CU
+      const int threads = 256, grid = cus * wps;
+      for (int rep = 0; rep < 2; ++rep) {
+        hipEventRecord(e0);
+        if (mode == 0)
+          hipLaunchKernelGGL(mfma_loop<0>, dim3(grid), dim3(threads), 0, 0, w, out, nblk);
+        else if (mode == 1)
+          hipLaunchKernelGGL(mfma_loop<1>, dim3(grid), dim3(threads), 0, 0, w, out, nblk);
+        else if (mode == 2)
+          hipLaunchKernelGGL(mfma_loop<2>, dim3(grid), dim3(threads), 0, 0, w, out, nblk);
+        else
+          hipLaunchKernelGGL(mfma_loop<3>, dim3(grid), dim3(threads), 0, 0, w, out, nblk);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+      }
+      float ms = 0;
+      hipEventElapsedTime(&ms, e0, e1);
+      const double flop = (double)grid * 4 * nblk * 16 * 2048.0;
+      const double tfs = flop / (ms * 1e-3) / 1e12;
+      const char* names[4] = {"registers", "A lds", "B global", "A lds + B global"};
+      printf("mode %s waves/SIMD %d: %.3f ms  %.1f TFLOP/s  frac %.3f\n", names[mode], wps, ms,
+             tfs, tfs / 157.3);
+    }
+  for (int wps : {1, 2}) {  // 512-thread workgroups: 2 waves per SIMD each; 1 or 2 per CU
+    const int grid = cus * wps, nchunk = 2048;
+    for (int rep = 0; rep < 2; ++rep) {
+      hipEventRecord(e0);
+      hipLaunchKernelGGL(wg_loop, dim3(grid), dim3(512), 0, 0, out, nchunk);
+      hipEventRecord(e1);
+      hipEventSynchronize(e1);
+    }
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    const double flop = (double)grid * 8 * nchunk * 32 * 4096.0;
+    const double tfs = flop / (ms * 1e-3) / 1e12;
+    printf("wgrad-shape 32x32x2 lds operands, waves/SIMD %d: %.3f ms  %.1f TFLOP/s  frac %.3f\n",
+           2 * wps, ms, tfs, tfs / 157.3);
+  }
+  hipFree(w);
+  hipFree(out);
+  return 0;
+}
