@@ -118,11 +118,20 @@ constexpr int kMaxRowS = 256;  // states dim bound of the fused path (LDS)
 #ifndef HWY_WG_DMA
 #define HWY_WG_DMA 1  // ppo_wgrad stages its chunks by LDS-DMA (wgrad_tile_dma); 0: register staging
 #endif
+#ifndef HWY_ROWS_C64
+#define HWY_ROWS_C64 1  // 64-row ppo_rows_c tiles at H = 256 (one workgroup per CU); 0: 32-row tiles
+#endif
 #ifndef HWY_WG_SPREAD
-#define HWY_WG_SPREAD 0  // 1: ppo_wgrad's LDS-DMA pieces issued between the MFMA groups
+// 1 (default): ppo_wgrad's LDS-DMA pieces for chunk c + 2 go out between chunk c's MFMA groups
+// instead of all six right after the barrier, where both waves of a SIMD issued them at once
+// (round 4: with HWY_RING_RA 203.4 -> 201.5 us per 16,384-row step, bit-identical weights)
+#define HWY_WG_SPREAD 1
 #endif
 #ifndef HWY_RING_RA
-#define HWY_RING_RA 0  // 1: the row kernels' activation reads pinned one block ahead
+// 1 (default): the row kernels' activation reads pinned one block ahead of their MFMAs (the
+// scheduler had sunk them to the end of the previous block, so every block opened on an LDS
+// wait); measured alone 203.4 -> 201.4 us per 16,384-row step, bit-identical weights
+#define HWY_RING_RA 1
 #endif
 #ifndef HWY_RING_DC
 #define HWY_RING_DC 2  // weight blocks in flight per wave in the compact-LDS ppo_rows
@@ -535,6 +544,9 @@ inline bool wg_balance_on() { return dev_knob_int("HWY_WG_BAL", 1) != 0; }
 // fit (H <= 256), else 16.
 inline int rows_tile(int B, int H) {
   if (H > 256) return kRowTile;
+  // 64-row tiles (ppo_rows_c64, one workgroup per CU) once every CU gets one: each weight
+  // fragment then feeds 4 row blocks, half the weight loads per MFMA of the 32-row tiles
+  if (HWY_ROWS_C64 && H == 256 && B >= 64 * chip_geom().cus) return 4 * kRowTile;
   const int force = dev_knob_int("HWY_ROWS_RT", 0);
   if (force == 16 || force == 32) return force;
   return B >= 32 * chip_geom().cus ? 2 * kRowTile : kRowTile;
@@ -1466,6 +1478,18 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2 
 ppo_rows_c(RowArgs r) {
   CLK_BEGIN
   rows_body<QH, NW, RT, true>(r);
+  CLK_END(0);
+}
+
+// the compact layout at 64-row tiles: 145 KB of LDS, one workgroup per CU (2 waves per SIMD,
+// up to 256 VGPRs).  An fp32 MFMA fed by global_load_dwordx4 weight fragments sustains ~75 % of
+// the matrix pipe at 8 MFMAs per fragment load (RB 2) and ~90 % at 16 (RB 4), 2 waves per SIMD
+// (tools/micro/mfma_f32_rate.hip); the 64-row tile buys the second ratio
+template <int QH, int NW>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4, 8)))
+ppo_rows_c64(RowArgs r) {
+  CLK_BEGIN
+  rows_body<QH, NW, 64, true>(r);
   CLK_END(0);
 }
 
@@ -2619,7 +2643,9 @@ int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
     r.counters = a->counters;
     // 8 waves (2 per SIMD) when the columns split into 16-wide tiles, else 4
     const dim3 g1(w.n1), b4(256), b8(512), blk(256);
-    if (w.rt == 2 * kRowTile) {
+    if (w.rt == 4 * kRowTile) {
+      hipLaunchKernelGGL((ppo_rows_c64<4, 8>), g1, b8, 0, s, r);
+    } else if (w.rt == 2 * kRowTile) {
       switch (H / 64) {
         case 1: hipLaunchKernelGGL((ppo_rows<1, 4, 32>), g1, b4, 0, s, r); break;
         case 2: hipLaunchKernelGGL((ppo_rows<2, 8, 32>), g1, b8, 0, s, r); break;
