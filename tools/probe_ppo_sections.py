@@ -42,7 +42,8 @@ torch.cuda.synchronize()
 L.hwy_ppo_debug_sections(buf, 1)
 steps = reps * nmb
 print(f"H={H}: {ev0.elapsed_time(ev1) / steps * 1e3:.1f} us per minibatch step (graph, incl. adam)")
-rt = int(os.environ.get("HWY_ROWS_RT", "0")) or (32 if H <= 256 and mb >= 8192 else 16)
+rt = int(os.environ.get("HWY_ROWS_RT", "0")) or (
+    64 if H == 256 and mb >= 64 * 256 else (32 if H <= 256 and mb >= 8192 else 16))
 n1 = (mb + rt - 1) // rt  # ppo_rows workgroups (rows_tile in ppo_kernels.hip)
 print(f"  ppo_rows: {rt} rows per workgroup, {n1} workgroups")
 names = {0: "rows: gather", 1: "rows: h1", 2: "rows: h2", 3: "rows: ac", 7: "rows: head sums",

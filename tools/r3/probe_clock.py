@@ -51,7 +51,8 @@ L.hwy_ppo_debug_wgtimes.argtypes = [ctypes.c_void_p]
 wt = (ctypes.c_ulonglong * (2 * 1024 * 3))()
 L.hwy_ppo_debug_wgtimes(wt)
 a = np.frombuffer(wt, dtype=np.uint64).reshape(2, 1024, 3).astype(np.int64)
-for k, name, nwg in ((0, "ppo_rows_c", mb // 32), (1, "ppo_wgrad", 269)):
+rt = 64 if mb >= 64 * 256 else 32  # ppo_rows_c64 / ppo_rows_c tiles at H 256
+for k, name, nwg in ((0, "ppo_rows_c", mb // rt), (1, "ppo_wgrad", 269)):
     t = a[k][:nwg]
     t = t[t[:, 1] > 0]
     t0, t1 = t[:, 0].min(), t[:, 1].max()
