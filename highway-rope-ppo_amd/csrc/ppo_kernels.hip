@@ -121,6 +121,9 @@ constexpr int kMaxRowS = 256;  // states dim bound of the fused path (LDS)
 #ifndef HWY_ROWS_C64
 #define HWY_ROWS_C64 1  // 64-row ppo_rows_c tiles at H = 256 (one workgroup per CU); 0: 32-row tiles
 #endif
+#ifndef HWY_WG_TEAMS
+#define HWY_WG_TEAMS 0  // 1: ppo_wgrad's row halves sync on LDS counters, not the chunk barrier
+#endif
 #ifndef HWY_WG_SPREAD
 // 1 (default): ppo_wgrad's LDS-DMA pieces for chunk c + 2 go out between chunk c's MFMA groups
 // instead of all six right after the barrier, where both waves of a SIMD issued them at once
@@ -1941,6 +1944,15 @@ typedef __attribute__((address_space(3))) void lds_void_t;
   float* b0 = wg_lds;
   float* b1 = wg_lds + BUF;
   float* b2 = wg_lds + 2 * BUF;
+  // HWY_WG_TEAMS: the two row halves of a chunk (waves 0-3: rows 0-31, waves 4-7: rows 32-63)
+  // touch disjoint LDS rows -- each half DMAs, and reads, only its own -- so each half
+  // synchronises on its own arrival counter in LDS instead of the workgroup barrier, and the two
+  // waves of a SIMD (one per half) drift out of step instead of meeting at every chunk's barrier
+  int* const team_cnt = reinterpret_cast<int*>(wg_lds + 3 * (kWgTM + kWgTN) * 64 + kWgWaves);
+  if (HWY_WG_TEAMS) {
+    if (t < 2) team_cnt[t] = 0;
+    __syncthreads();
+  }
   // earlier stores of this wave (a previous tile's partial) drained: the vmcnt counts are exact
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   dma(0, b0);
@@ -1955,7 +1967,24 @@ typedef __attribute__((address_space(3))) void lds_void_t;
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if (HWY_WG_TEAMS) {
+      // arrive (this wave's DMA of chunk c has landed and its reads of chunk c - 1 returned),
+      // then wait for the other three waves of the half: every chunk raises the count by 4
+      // (inline asm: as C++ atomics the compiler orders them behind every LDS-DMA in flight,
+      // s_waitcnt vmcnt(0), which would drain chunk c + 1's prefetch)
+      const uint32_t ca = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int*)(team_cnt + kh);
+      if (lane == 0) asm volatile("ds_add_u32 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(ca), "v"(1) : "memory");
+      const int target = 4 * (c + 1);
+      for (;;) {
+        int seen;
+        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(seen) : "v"(ca) : "memory");
+        if (__builtin_amdgcn_readfirstlane(seen) >= target) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      __builtin_amdgcn_s_barrier();
+    }
     // chunk c + 2 into chunk c - 1's buffer: here, or spread between this chunk's MFMA groups
     if (!HWY_WG_SPREAD && c + 2 < nchunk) dma(c + 2, b2);
     compute(b0, kb1 - (kb0 + 64 * c), mask_tag, c + 2 < nchunk ? c + 2 : -1, b2);
@@ -2218,7 +2247,7 @@ __device__ __forceinline__ void ppo_wgrad_body(const WgArgs& a) {
   // drain every DMA before the first operand read of a chunk): the chunk buffers, then the
   // reduction slots
   constexpr int kWgBufs = HWY_WG_DMA ? 3 : 2;
-  __shared__ __attribute__((aligned(16))) float wg_lds[kWgBufs * (kWgTM + kWgTN) * 64 + kWgWaves];
+  __shared__ __attribute__((aligned(16))) float wg_lds[kWgBufs * (kWgTM + kWgTN) * 64 + kWgWaves + 2];
   float* red = wg_lds + kWgBufs * (kWgTM + kWgTN) * 64;
   const int ntile = a.tac + a.t2 + a.t1;
   const int id = blockIdx.x;
@@ -2268,14 +2297,22 @@ __global__ void __launch_bounds__(512) ppo_wgrad(WgArgs a) {
   CLK_END(1);
 }
 
-// ppo_wsum: the split partial tiles of every weight-gradient tile summed in split order
-// (deterministic) into the flat gradient, 1024 elements (16 tile rows) per workgroup with all
-// splits' float4s in flight per thread, the bias sums, and one sum-of-squares partial each.
-__global__ void __launch_bounds__(256) ppo_wsum(WgArgs a) {
-  __shared__ float red[4];
+// One ppo_wsum work item (1024 elements of a weight-gradient tile, 16 tile rows): the split
+// partial tiles summed in split order (deterministic) into the flat gradient, with all splits'
+// float4s in flight per thread, the bias sums of the tile's rows (work item 0 of the tile's
+// first column), and this thread's sum of squares.  gi / bi: the flat indices written (-1: none).
+struct WsumItem {
+  f32x4 v;
+  int64_t gi[4];
+  float b;
+  int64_t bi;
+  float sq;
+};
+
+__device__ __forceinline__ void wsum_item(const WgArgs& a, int item, WsumItem& it) {
   const int t = threadIdx.x, H = a.H;
   constexpr int kParts = kWgTM * kWgTN / 1024;
-  const int tile_id = blockIdx.x / kParts, part = blockIdx.x % kParts;
+  const int tile_id = item / kParts, part = item % kParts;
   int id = tile_id, M, N, region;
   if (id < a.tac) {
     M = 2 * H, N = H, region = 0;
@@ -2311,15 +2348,22 @@ __global__ void __launch_bounds__(256) ppo_wsum(WgArgs a) {
   for (int q = 1; q < kMaxParts; ++q)
     if (q < np) v += pv[q];
   float sq = 0.0f;
+  it.v = v;
+#pragma unroll
+  for (int c4 = 0; c4 < 4; ++c4) it.gi[c4] = -1;
   if (i0 + ri < M) {
-    float* dst = a.grads + grad_row(i0 + ri) + j0 + cj;
+    const long row = grad_row(i0 + ri) + j0 + cj;
+    float* dst = a.grads + row;
 #pragma unroll
     for (int c4 = 0; c4 < 4; ++c4)
       if (j0 + cj + c4 < N) {
         dst[c4] = v[c4];
         sq += v[c4] * v[c4];
+        it.gi[c4] = row + c4;
       }
   }
+  it.b = 0.0f;
+  it.bi = -1;
   if (bias_t) {  // bias of output row i0 + t
     float b = 0.0f;
 #pragma unroll
@@ -2332,9 +2376,19 @@ __global__ void __launch_bounds__(256) ppo_wsum(WgArgs a) {
     else bo = a.off[P_B1] + i;
     a.grads[bo] = b;
     sq += b * b;
+    it.b = b;
+    it.bi = bo;
   }
-  const float tot = block_sum4(sq, red);
-  if (t == 0) a.norm_part[a.nh + blockIdx.x] = tot;
+  it.sq = sq;
+}
+
+// ppo_wsum: every work item of every weight-gradient tile, one sum-of-squares partial each
+__global__ void __launch_bounds__(256) ppo_wsum(WgArgs a) {
+  __shared__ float red[4];
+  WsumItem it;
+  wsum_item(a, blockIdx.x, it);
+  const float tot = block_sum4(it.sq, red);
+  if (threadIdx.x == 0) a.norm_part[a.nh + blockIdx.x] = tot;
 }
 
 // ----------------------------------------------------------------------------- reduce
@@ -2516,18 +2570,9 @@ __global__ void __launch_bounds__(kRedThreads) ppo_sumsq(const float* g, int64_t
 #endif
 constexpr int kAdamEPT = HWY_ADAM_EPT;  // elements per thread (same box: 1 5.9 µs, 2 5.5, 4 5.7, 8 7.4)
 
-__global__ void __launch_bounds__(256) ppo_adam(OptArgs o) {
-  __shared__ float red[4];
-  __shared__ float coef_s, step_s, bc2s_s;
-  // this thread's elements first (256 apart, coalesced): their loads overlap the norm
-  // reduction's
-  float g_raw[kAdamEPT], m_old[kAdamEPT], v_old[kAdamEPT], p_old[kAdamEPT];
-#pragma unroll
-  for (int q = 0; q < kAdamEPT; ++q) {
-    const int64_t i = ((int64_t)blockIdx.x * kAdamEPT + q) * 256 + threadIdx.x;
-    const int64_t ii = i < o.numel ? i : 0;
-    g_raw[q] = o.grads[ii], m_old[q] = o.m[ii], v_old[q] = o.v[ii], p_old[q] = o.params[ii];
-  }
+// clip_grad_norm_'s coefficient from the norm partials and Adam's bias corrections, into
+// sh[0] (coef), sh[1] (lr / bc1), sh[2] (sqrt bc2); every thread of the workgroup calls it
+__device__ __forceinline__ void adam_scalars(const OptArgs& o, float* red, float* sh) {
   float s = 0.0f;
   for (int k = threadIdx.x; k < o.nred; k += 256) s += o.norm_part[k];
   s = wave_sum_dpp(s);
@@ -2543,32 +2588,52 @@ __global__ void __launch_bounds__(256) ppo_adam(OptArgs o) {
     }
     const double bc1 = 1.0 - p1;
     const double bc2 = 1.0 - p2;
-    step_s = (float)((double)o.lr / bc1);
-    bc2s_s = (float)sqrt(bc2);
+    sh[1] = (float)((double)o.lr / bc1);
+    sh[2] = (float)sqrt(bc2);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     const float total = sqrtf(((red[0] + red[1]) + red[2]) + red[3]);
     const float c = o.max_norm / (total + 1e-6f);
-    coef_s = c < 1.0f ? c : 1.0f;
+    sh[0] = c < 1.0f ? c : 1.0f;
   }
   __syncthreads();
-  const float coef = coef_s;
-  const float step_size = step_s, bc2_sqrt = bc2s_s;
+}
+
+// one element of torch.optim.Adam after the clip (parameter i, its raw gradient and old state)
+__device__ __forceinline__ void adam_elem(const OptArgs& o, int64_t i, float g_raw, float m_old,
+                                          float v_old, float p_old, const float* sh) {
+  const float coef = sh[0], step_size = sh[1], bc2_sqrt = sh[2];
+  const float g = g_raw * coef;
+  float mm = m_old, vv = v_old;
+  mm = mm + (1.0f - o.beta1) * (g - mm);  // exp_avg.lerp_(grad, 1 - beta1)
+  vv = vv * o.beta2 + (1.0f - o.beta2) * g * g;
+  o.m[i] = mm;
+  o.v[i] = vv;
+  const float denom = sqrtf(vv) / bc2_sqrt + o.eps;
+  const float pn = p_old - step_size * (mm / denom);
+  o.params[i] = pn;
+  if (o.tiles) write_tiles(o, i, pn);
+}
+
+__global__ void __launch_bounds__(256) ppo_adam(OptArgs o) {
+  __shared__ float red[4];
+  __shared__ float sh[3];
+  // this thread's elements first (256 apart, coalesced): their loads overlap the norm
+  // reduction's
+  float g_raw[kAdamEPT], m_old[kAdamEPT], v_old[kAdamEPT], p_old[kAdamEPT];
+#pragma unroll
+  for (int q = 0; q < kAdamEPT; ++q) {
+    const int64_t i = ((int64_t)blockIdx.x * kAdamEPT + q) * 256 + threadIdx.x;
+    const int64_t ii = i < o.numel ? i : 0;
+    g_raw[q] = o.grads[ii], m_old[q] = o.m[ii], v_old[q] = o.v[ii], p_old[q] = o.params[ii];
+  }
+  adam_scalars(o, red, sh);
 #pragma unroll
   for (int q = 0; q < kAdamEPT; ++q) {
     const int64_t i = ((int64_t)blockIdx.x * kAdamEPT + q) * 256 + threadIdx.x;
     if (i >= o.numel) break;
-    const float g = g_raw[q] * coef;
-    float mm = m_old[q], vv = v_old[q];
-    mm = mm + (1.0f - o.beta1) * (g - mm);  // exp_avg.lerp_(grad, 1 - beta1)
-    vv = vv * o.beta2 + (1.0f - o.beta2) * g * g;
-    o.m[i] = mm;
-    o.v[i] = vv;
-    const float denom = sqrtf(vv) / bc2_sqrt + o.eps;
-    const float pn = p_old[q] - step_size * (mm / denom);
-    o.params[i] = pn;
-    if (o.tiles) write_tiles(o, i, pn);
+    adam_elem(o, i, g_raw[q], m_old[q], v_old[q], p_old[q], sh);
   }
 }
 
