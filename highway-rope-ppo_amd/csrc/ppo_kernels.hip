@@ -119,7 +119,9 @@ constexpr int kMaxRowS = 256;  // states dim bound of the fused path (LDS)
 #define HWY_WG_DMA 1  // ppo_wgrad stages its chunks by LDS-DMA (wgrad_tile_dma); 0: register staging
 #endif
 #ifndef HWY_ROWS_R
-#define HWY_ROWS_R 1  // 64-row tiles at H = 256 run ppo_rows_r (activations in registers); 0: ppo_rows_c64
+// 64-row tiles at H = 256: 2 ppo_rows_k (activations in registers, split-K wave pairs), 1 ppo_rows_r
+// (activations in registers, one wave per SIMD), 0 ppo_rows_c64
+#define HWY_ROWS_R 2
 #endif
 #ifndef HWY_ROWS_C64
 #define HWY_ROWS_C64 1  // 64-row ppo_rows_c tiles at H = 256 (one workgroup per CU); 0: 32-row tiles
@@ -2112,8 +2114,397 @@ ppo_rows_r(RowArgs r) {
   CLK_END(0);
 }
 
-// ppo_act_r: ActorCritic.act with ppo_rows_r's forward bits (H = 256), for acting between
-// updates whose minibatch step runs ppo_rows_r.  Every output element is the same chain of MFMAs
+// ----------------------------------------------------------------------------- ppo_rows_k
+// ppo_rows_r's transposed, register-chained layers at two waves per SIMD (ppo_rows_r's single wave
+// per SIMD left the matrix pipe idle through every wait: MFMA busy 0.58 against ppo_rows_c64's
+// 0.68).  8 waves: wave w owns the 16 rows of row block w & 3 and the k-blocks of parity
+// h = w >> 2 of every layer (split-K; waves w and w + 4 share a SIMD).  Each wave accumulates all 16
+// output tiles over its half of the reduction; at a layer's end the two waves of a row block swap
+// the partial sums of each other's parity through LDS (8 tiles each way) and each finishes the 8
+// output tiles of its own parity -- acc_even + acc_odd, bias, ReLU, stores -- which are exactly its
+// B operands (the k-blocks of its parity) for the next layer.  The loss head's dot products are
+// summed per parity, then added; dL/d[a1|c1] of a wave's own tiles is its B operand for dh2 as
+// computed, so the head needs no tile exchange.  Ring: 2 slots of 2 k-blocks x 16 tiles (each wave
+// reads the k-block of its parity, DMAs 4 tiles), one barrier per slot; a layer boundary's
+// exchange, epilogue and stores run after the next slot's barrier, before that slot's DMA.
+constexpr int kRkWaves = 8;
+constexpr int kRkRows = 64;
+constexpr int kRkDma = 2 * 16 / kRkWaves;
+// LDS (floats): ring (2 slots) | exchange [8 waves][8 tiles][64 lanes] f32x4 | b1 b2 ba1 bc1 |
+// wa2 row 0, row 1, wc2 | head dot-product exchange [8 waves][16 rows] f32x4 | head combine
+// [8 waves][3 x 128 column sums + 16 tail sums]
+constexpr int kRkLdsX = 2 * kRrSlotF;
+constexpr int kRkLdsBias = kRkLdsX + kRkWaves * 8 * 64 * 4;
+constexpr int kRkLdsHw = kRkLdsBias + 4 * 256;
+constexpr int kRkLdsP = kRkLdsHw + 3 * 256;
+constexpr int kRkComb = 3 * 128 + 16;
+constexpr int kRkLdsComb = kRkLdsP + kRkWaves * 16 * 4;
+constexpr int kRkLdsF = kRkLdsComb + kRkWaves * kRkComb;
+static_assert(kRkLdsF * 4 <= 160 * 1024, "ppo_rows_k LDS");
+
+// this wave's 4 tiles of slot q: k-block h of the slot, output tiles 4 (w & 3) .. + 3
+template <int SB>
+__device__ __forceinline__ void rk_dma(float* lds, const float* tiles, int q, int w, int lane) {
+  float* slot = lds + (q & 1) * kRrSlotF;
+  const int kbl = w >> 2;
+#pragma unroll
+  for (int i = 0; i < kRkDma; ++i) {
+    const int nb = 4 * (w & 3) + i;
+    __builtin_amdgcn_global_load_lds((const void*)(rr_tile<SB>(tiles, q, kbl, nb) + 4 * lane),
+                                     (lds_void_t*)(slot + (kbl * 16 + nb) * 256), 16, 0, 0);
+  }
+}
+
+// acc[nb] += W(k-block tiles)[nb] x b over one k-block (16 tiles at kt, 4 groups of 4, each
+// group's fragment reads issued before the previous group's MFMAs)
+__device__ __forceinline__ void rk_mma(const float* kt, int lane, const f32x4& b,
+                                       f32x4 (&acc)[16]) {
+  const float* base = kt + 4 * lane;
+  f32x4 a[2][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a[0][i] = *reinterpret_cast<const f32x4*>(base + i * 256);
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    const int cur = g4 & 1;
+    if (g4 + 1 < 4) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a[cur ^ 1][i] = *reinterpret_cast<const f32x4*>(base + (4 * (g4 + 1) + i) * 256);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        acc[4 * g4 + i] =
+            __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][i][j], b[j], acc[4 * g4 + i], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// slot Q: its DMAs (issued one slot ago) landed for every wave (nothing younger is in flight: the
+// stores of a layer boundary go out before the next DMA), then `pre` (a layer boundary's work),
+// then the DMA of slot Q + 1 into the other buffer, then this wave's MFMAs
+template <int SB, int NS, int Q, class PRE>
+__device__ __forceinline__ void rk_slot(float* lds, const float* tiles, int w, int lane,
+                                        const f32x4& b, f32x4 (&acc)[16], PRE&& pre) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  pre();
+  if constexpr (Q + 1 < NS) rk_dma<SB>(lds, tiles, Q + 1, w, lane);
+  rk_mma(lds + (Q & 1) * kRrSlotF + (w >> 2) * 16 * 256, lane, b, acc);
+}
+
+// slots Q0 .. Q0 + NQ - 1 with this wave's B operands bh[s]; `pre` runs in the first slot
+template <int SB, int NS, int Q0, int NQ, class PRE>
+__device__ __forceinline__ void rk_layer(float* lds, const float* tiles, int w, int lane,
+                                         const f32x4 (&bh)[NQ], f32x4 (&acc)[16], PRE&& pre) {
+  static_for<0, NQ>([&](auto si) {
+    constexpr int s = decltype(si)::value;
+    if constexpr (s == 0)
+      rk_slot<SB, NS, Q0 + s>(lds, tiles, w, lane, bh[s], acc, pre);
+    else
+      rk_slot<SB, NS, Q0 + s>(lds, tiles, w, lane, bh[s], acc, [] {});
+  });
+}
+
+// the partner's (other parity) half of a layer boundary: this wave's partial sums of the tiles of
+// the other parity into the exchange image
+__device__ __forceinline__ void rk_put(float* lds, int w, int lane, const f32x4 (&acc)[16]) {
+  f32x4* X = reinterpret_cast<f32x4*>(lds + kRkLdsX) + w * 8 * 64;
+  const bool odd = (w >> 2) == 0;  // the partner's parity (a select: no run-time register index)
+#pragma unroll
+  for (int i = 0; i < 8; ++i) X[i * 64 + lane] = odd ? acc[2 * i + 1] : acc[2 * i];
+}
+// this wave's own tiles (2 i + h): its partial + the partner's
+__device__ __forceinline__ void rk_get(const float* lds, int w, int lane, const f32x4 (&acc)[16],
+                                       f32x4 (&out)[8]) {
+  const f32x4* X = reinterpret_cast<const f32x4*>(lds + kRkLdsX) + (w ^ 4) * 8 * 64;
+  const bool odd = (w >> 2) != 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) out[i] = (odd ? acc[2 * i + 1] : acc[2 * i]) + X[i * 64 + lane];
+}
+// bias + ReLU of the own tiles (nb = 2 i + h), their ReLU decisions as bits 4 i + r
+__device__ __forceinline__ uint32_t rk_bias_relu(f32x4 (&v)[8], const float* bias, int h, int g) {
+  uint32_t m = 0u;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + 16 * (2 * i + h) + 4 * g);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float x = v[i][r] + bv[r];
+      x = x > 0.0f ? x : 0.0f;
+      v[i][r] = x;
+      m |= (x > 0.0f ? 1u : 0u) << (4 * i + r);
+    }
+  }
+  return m;
+}
+__device__ __forceinline__ void rk_mask(f32x4 (&v)[8], uint32_t m) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[i][r] = ((m >> (4 * i + r)) & 1u) ? v[i][r] : 0.0f;
+}
+__device__ __forceinline__ void rk_store(float* dst, long ld, bool live, int h, int g, int c,
+                                         const f32x4 (&v)[8]) {
+  if (!live) return;
+  float* p = dst + (long)c * ld + 4 * g;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) *reinterpret_cast<f32x4*>(p + 16 * (2 * i + h)) = v[i];
+}
+__device__ __forceinline__ void rk_zero(f32x4 (&acc)[16]) {
+#pragma unroll
+  for (int nb = 0; nb < 16; ++nb) acc[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+}
+
+template <int SB>
+__global__ void __launch_bounds__(64 * kRkWaves) __attribute__((amdgpu_waves_per_eu(2, 2)))
+ppo_rows_k(RowArgs r) {
+  constexpr int H = 256;
+  constexpr int NS = SB / 2 + 48;
+  constexpr int Q2 = SB / 2, QA = Q2 + 8, QC = QA + 8, QBA = QC + 8, QBC = QBA + 8, QB2 = QBC + 8;
+  __shared__ __attribute__((aligned(16))) float lds[kRkLdsF];
+  CLK_BEGIN
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, g = lane >> 4, c = lane & 15;
+  const int rb = w & 3, h = w >> 2;
+  const int S = r.S;
+  const int row0 = blockIdx.x * kRkRows;
+  const int nrows = min(kRkRows, r.B - row0);
+  const int wr0 = row0 + 16 * rb;           // this wave's first row
+  const bool live = 16 * rb + c < nrows;    // this lane's row exists
+  const float* P = r.params;
+  const float* tiles = r.tiles;
+  if (blockIdx.x == 0 && t == 0) {
+    r.counters[0] += 1;  // Adam step t for this minibatch
+    r.counters[1] += 1;  // metrics row (this step writes row counters[1]-1)
+  }
+  // ---- plain global loads first, all consumed before the first LDS-DMA (hipcc waits vmcnt(0)
+  // at the use of an ordinary load while an LDS-DMA is in flight)
+  const long src = (long)r.idx[live ? wr0 + c : row0];
+  f32x4 x[SB / 2];  // layer 1's B operands: the states row's k-blocks 2 i + h
+#pragma unroll
+  for (int i = 0; i < SB / 2; ++i) {
+    const int k = 16 * (2 * i + h) + 4 * g;
+    x[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (live && k < S) x[i] = *reinterpret_cast<const f32x4*>(r.states + src * S + k);
+  }
+  const float hz0 = r.pre_tanh[src * 2], hz1 = r.pre_tanh[src * 2 + 1];
+  const float hold = r.old_logp[src], hadv = r.adv[src], hret = r.ret[src];
+  for (int e = t; e < 4 * 256; e += 64 * kRkWaves) {
+    const int l = e >> 8, n = e & 255;
+    const int64_t bo = l == 0 ? r.off[P_B1] : l == 1 ? r.off[P_B2] : l == 2 ? r.off[P_BA1] : r.off[P_BC1];
+    lds[kRkLdsBias + e] = P[bo + n];
+  }
+  for (int e = t; e < 3 * 256; e += 64 * kRkWaves) {
+    const int l = e >> 8, n = e & 255;
+    lds[kRkLdsHw + e] = P[(l == 2 ? r.off[P_WC2] : r.off[P_WA2] + l * H) + n];
+  }
+  if (live) {
+#pragma unroll
+    for (int i = 0; i < SB / 2; ++i) {
+      const int k = 16 * (2 * i + h) + 4 * g;
+      if (k < S) *reinterpret_cast<f32x4*>(r.xg + (long)(wr0 + c) * S + k) = x[i];
+    }
+  }
+  const float ba0 = P[r.off[P_BA2]], ba1 = P[r.off[P_BA2] + 1], bcv = P[r.off[P_BC2]];
+  const float ls0 = P[r.off[P_LOGSTD]], ls1 = P[r.off[P_LOGSTD] + 1];
+  // the squash correction of the stored pre-tanh actions, off the head's dependent chain
+  const float hq0 = log1pf(-(tanhf(hz0) * tanhf(hz0)) + 1e-6f);
+  const float hq1 = log1pf(-(tanhf(hz1) * tanhf(hz1)) + 1e-6f);
+  // every ordinary load has returned before the first LDS-DMA goes out
+  asm volatile("" ::"v"(hold), "v"(hadv), "v"(hret), "v"(hq0), "v"(hq1), "v"(ba0), "v"(ba1),
+               "v"(bcv), "v"(ls0), "v"(ls1)
+               : "memory");
+  __syncthreads();  // the bias / head-weight tables (no LDS-DMA in flight yet)
+  rk_dma<SB>(lds, tiles, 0, w, lane);
+  const float* bias = lds + kRkLdsBias;
+
+  f32x4 acc[16];
+  f32x4 v1[8], v2[8], a1[8], c1[8];
+  uint32_t m1 = 0u, m2 = 0u;
+  // ---- h1 = relu(W1 x + b1)
+  rk_zero(acc);
+  rk_layer<SB, NS, 0, SB / 2>(lds, tiles, w, lane, x, acc, [] {});
+  rk_put(lds, w, lane, acc);
+  // ---- h2 = relu(W2 h1 + b2); the boundary (h1's exchange, epilogue, stores) in its first slot
+  {
+    f32x4 acc2[16];
+    rk_zero(acc2);
+    rk_layer<SB, NS, Q2, 8>(lds, tiles, w, lane, v1, acc2, [&] {
+      rk_get(lds, w, lane, acc, v1);
+      m1 = rk_bias_relu(v1, bias, h, g);
+      rk_store(r.h1 + (long)wr0 * H, H, live, h, g, c, v1);
+    });
+    rk_put(lds, w, lane, acc2);
+#pragma unroll
+    for (int nb = 0; nb < 16; ++nb) acc[nb] = acc2[nb];
+  }
+  // ---- a1 = relu(Wa1 h2 + ba1), c1 = relu(Wc1 h2 + bc1)
+  {
+    f32x4 acc2[16];
+    rk_zero(acc2);
+    rk_layer<SB, NS, QA, 8>(lds, tiles, w, lane, v2, acc2, [&] {
+      rk_get(lds, w, lane, acc, v2);
+      m2 = rk_bias_relu(v2, bias + 256, h, g);
+      rk_store(r.h2 + (long)wr0 * H, H, live, h, g, c, v2);
+    });
+    rk_put(lds, w, lane, acc2);
+    rk_zero(acc);
+    rk_layer<SB, NS, QC, 8>(lds, tiles, w, lane, v2, acc, [&] {
+      rk_get(lds, w, lane, acc2, a1);
+      (void)rk_bias_relu(a1, bias + 512, h, g);
+    });
+    rk_put(lds, w, lane, acc);
+  }
+  // ---- loss head (ppo/agent.py:226-245), at the first dh2 slot's boundary: c1's exchange, the
+  // dot products per parity (then the pair's sum), the per-row scalars, dL/d[a1 | c1] of the own
+  // tiles (dh2's B operands), the head-weight gradient column sums into the combine image
+  const float* wa0 = lds + kRkLdsHw;
+  const float* wa1 = wa0 + 256;
+  const float* wcv = wa0 + 512;
+  float tl[9];
+  auto head = [&] {
+    rk_get(lds, w, lane, acc, c1);
+    (void)rk_bias_relu(c1, bias + 768, h, g);
+    float p0 = 0.0f, p1 = 0.0f, pv = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int o = 16 * (2 * i + h) + 4 * g;
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(wa0 + o);
+      const f32x4 x1 = *reinterpret_cast<const f32x4*>(wa1 + o);
+      const f32x4 xc = *reinterpret_cast<const f32x4*>(wcv + o);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        p0 += a1[i][q] * x0[q];
+        p1 += a1[i][q] * x1[q];
+        pv += c1[i][q] * xc[q];
+      }
+    }
+    p0 += __shfl_xor(p0, 16), p1 += __shfl_xor(p1, 16), pv += __shfl_xor(pv, 16);
+    p0 += __shfl_xor(p0, 32), p1 += __shfl_xor(p1, 32), pv += __shfl_xor(pv, 32);
+    f32x4* PX = reinterpret_cast<f32x4*>(lds + kRkLdsP);
+    if (g == 0) PX[w * 16 + c] = f32x4{p0, p1, pv, 0.0f};
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const f32x4 po = PX[(w ^ 4) * 16 + c];
+    p0 = p0 + po[0], p1 = p1 + po[1], pv = pv + po[2];  // the even + odd parity sums (commutative)
+    // torch Normal: scale = exp(log_std); var = scale**2; log_scale = log(scale)
+    const float sc0 = expf(ls0), sc1 = expf(ls1);
+    const float var0 = sc0 * sc0, var1 = sc1 * sc1;
+    const float lsc0 = logf(sc0), lsc1 = logf(sc1);
+    const float LOG_SQRT_2PI = 0.91893853320467274178f;
+    const float invB = 1.0f / (float)r.B;
+    const float lo = 1.0f - r.eps_clip, hi = 1.0f + r.eps_clip;
+    const float mu0 = p0 + ba0, mu1 = p1 + ba1, val = pv + bcv;
+    const float d0 = hz0 - mu0, d1 = hz1 - mu1;
+    const float lp0 = -(d0 * d0) / (2.0f * var0) - lsc0 - LOG_SQRT_2PI;
+    const float lp1 = -(d1 * d1) / (2.0f * var1) - lsc1 - LOG_SQRT_2PI;
+    const float logp = (lp0 - hq0) + (lp1 - hq1);
+    const float log_ratio = logp - hold;
+    const float ratio = expf(log_ratio);
+    const float cr = fminf(fmaxf(ratio, lo), hi);
+    const float s1 = ratio * hadv, s2 = cr * hadv;
+    const float inr = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
+    // torch.min / clamp backward: ties split the gradient evenly
+    const float wsel = s1 < s2 ? 1.0f : (s1 > s2 ? inr : 0.5f * (1.0f + inr));
+    const float dlogp = -invB * hadv * wsel * ratio;  // d(actor_loss)/d(logp)
+    const float dmu0 = live ? dlogp * d0 / var0 : 0.0f;
+    const float dmu1 = live ? dlogp * d1 / var1 : 0.0f;
+    const float dv = live ? r.value_coef * 2.0f * (val - hret) * invB : 0.0f;
+    tl[0] = dmu0, tl[1] = dmu1, tl[2] = dv;
+    tl[3] = live ? dlogp * ((d0 * d0) / var0 - 1.0f) : 0.0f;
+    tl[4] = live ? dlogp * ((d1 * d1) / var1 - 1.0f) : 0.0f;
+    tl[5] = live ? -fminf(s1, s2) : 0.0f;
+    tl[6] = live ? (val - hret) * (val - hret) : 0.0f;
+    tl[7] = live ? (fabsf(ratio - 1.0f) > r.eps_clip ? 1.0f : 0.0f) : 0.0f;
+    tl[8] = live ? (ratio - 1.0f) - log_ratio : 0.0f;
+    float* comb = lds + kRkLdsComb + w * kRkComb;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int o = 16 * (2 * i + h) + 4 * g;
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(wa0 + o);
+      const f32x4 x1 = *reinterpret_cast<const f32x4*>(wa1 + o);
+      const f32x4 xc = *reinterpret_cast<const f32x4*>(wcv + o);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float a = a1[i][q], cc = c1[i][q];
+        const float s0 = row16_sum(dmu0 * a), s1v = row16_sum(dmu1 * a), sc = row16_sum(dv * cc);
+        if (c == 0) {
+          const int nl = 16 * i + 4 * g + q;  // column 16 (2 i + h) + 4 g + q among this parity's
+          comb[nl] = s0;
+          comb[128 + nl] = s1v;
+          comb[256 + nl] = sc;
+        }
+        a1[i][q] = a > 0.0f ? (dmu0 * x0[q] + dmu1 * x1[q]) : 0.0f;
+        c1[i][q] = cc > 0.0f ? dv * xc[q] : 0.0f;
+      }
+    }
+    if (h == 0) {  // the row scalars once per row block (both waves of a pair hold them)
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const float v = row16_sum(tl[k]);
+        if (lane == k) comb[384 + k] = v;  // lane k < 16 is in DPP row 0 (g = 0)
+      }
+    }
+    rk_store(r.dac + (long)wr0 * 2 * H, 2 * H, live, h, g, c, a1);
+    rk_store(r.dac + (long)wr0 * 2 * H + H, 2 * H, live, h, g, c, c1);
+  };
+  // ---- dh2 = (dac [Wa1; Wc1]) * (h2 > 0); the head partial row of the workgroup (the combine
+  // image complete behind the second dh2 slot's barrier) in that slot
+  {
+    f32x4 acc2[16];
+    rk_zero(acc2);
+    static_for<0, 8>([&](auto si) {
+      constexpr int s = decltype(si)::value;
+      if constexpr (s == 0) {
+        rk_slot<SB, NS, QBA>(lds, tiles, w, lane, a1[0], acc2, head);
+      } else if constexpr (s == 1) {
+        rk_slot<SB, NS, QBA + 1>(lds, tiles, w, lane, a1[1], acc2, [&] {
+          float* out = r.head_part + (long)blockIdx.x * r.HP;
+          const float* cb = lds + kRkLdsComb;
+          for (int e = t; e < 3 * H + 9; e += 64 * kRkWaves) {
+            int hh = 0, o;
+            if (e < 3 * H) {
+              const int k = e >> 8, n = e & 255;
+              hh = (n >> 4) & 1;
+              o = 128 * k + 16 * (n >> 5) + (n & 15);
+            } else {
+              o = 384 + (e - 3 * H);
+            }
+            float v = cb[(4 * hh) * kRkComb + o];
+#pragma unroll
+            for (int q = 1; q < 4; ++q) v += cb[(q + 4 * hh) * kRkComb + o];
+            out[e] = v;
+          }
+        });
+      } else {
+        rk_slot<SB, NS, QBA + s>(lds, tiles, w, lane, a1[s], acc2, [] {});
+      }
+    });
+    rk_layer<SB, NS, QBC, 8>(lds, tiles, w, lane, c1, acc2, [] {});
+    rk_put(lds, w, lane, acc2);
+    // ---- dh1 = (dh2 W2) * (h1 > 0)
+    rk_zero(acc);
+    rk_layer<SB, NS, QB2, 8>(lds, tiles, w, lane, v2, acc, [&] {
+      rk_get(lds, w, lane, acc2, v2);
+      rk_mask(v2, m2);
+      rk_store(r.dh2 + (long)wr0 * H, H, live, h, g, c, v2);
+    });
+  }
+  rk_put(lds, w, lane, acc);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  rk_get(lds, w, lane, acc, v1);
+  rk_mask(v1, m1);
+  rk_store(r.dh1 + (long)wr0 * H, H, live, h, g, c, v1);
+  CLK_END(0);
+}
+
+// ppo_act_r: ActorCritic.act with the forward bits of the register row kernels (H = 256:
+// ppo_rows_k, or ppo_rows_r when HWY_ROWS_R == 1), for acting between updates whose minibatch
+// step runs them.  Every output element is the same chain of MFMAs
 // (weights as the A operand, k-blocks and k-steps in the same order, from zero), the same bias +
 // ReLU and the same head dot products and lane sums, so mean / value / log-prob are the bits the
 // step recomputes (ratio exactly 1 on the acted rows).  The work is split the other way round
@@ -2123,7 +2514,7 @@ ppo_rows_r(RowArgs r) {
 // (global loads, 4 k-blocks ahead).  Wave 0 runs the head of all 16 rows.
 constexpr int kArD = 4;  // k-blocks of weight fragments in flight per wave
 __device__ __forceinline__ void ar_layer(const float* seg, int nblk, const f32x4* bimg, int lane,
-                                         int w, f32x4 (&acc)[4]) {
+                                         int w, f32x4 (&acc)[4], f32x4 (&acc_o)[4]) {
   const float* base = seg + (long)(4 * w) * nblk * 256 + 4 * lane;  // tile (4 w, 0), this lane
   f32x4 ring[kArD][4];
 #pragma unroll
@@ -2136,11 +2527,13 @@ __device__ __forceinline__ void ar_layer(const float* seg, int nblk, const f32x4
     for (int d = 0; d < kArD; ++d) {
       const int kb = kb0 + d;
       const f32x4 b = bimg[kb * 64 + lane];
+      // ppo_rows_k: the even and the odd k-blocks in separate sums (kb0 % 4 == 0: parity of d)
+      f32x4 (&ac)[4] = (HWY_ROWS_R == 2 && (d & 1)) ? acc_o : acc;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(ring[d][i][j], b[j], acc[i], 0, 0, 0);
+          ac[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(ring[d][i][j], b[j], ac[i], 0, 0, 0);
       const int kn = min(kb + kArD, nblk - 1);  // past the end: an in-range tile, never used
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -2150,20 +2543,21 @@ __device__ __forceinline__ void ar_layer(const float* seg, int nblk, const f32x4
 }
 
 // bias + ReLU (rr_bias_relu's expression) of this wave's 4 output tiles into image `out`
-__device__ __forceinline__ void ar_epi(f32x4 (&acc)[4], const float* bias, f32x4* out, int w,
-                                       int lane) {
+__device__ __forceinline__ void ar_epi(f32x4 (&acc)[4], f32x4 (&acc_o)[4], const float* bias,
+                                       f32x4* out, int w, int lane) {
   const int g = lane >> 4;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int nb = 4 * w + i;
     const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + 16 * nb + 4 * g);
+    if (HWY_ROWS_R == 2) acc[i] = acc[i] + acc_o[i];  // ppo_rows_k's even + odd partial sums
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const float v = acc[i][q] + bv[q];
       acc[i][q] = v > 0.0f ? v : 0.0f;
     }
     out[nb * 64 + lane] = acc[i];
-    acc[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    acc[i] = acc_o[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
   }
 }
 
@@ -2195,38 +2589,51 @@ __global__ void __launch_bounds__(256) ppo_act_r(ActArgs r) {
     img[1][kb * 64 + lane] = v;
   }
   __syncthreads();
-  f32x4 acc[4];
+  f32x4 acc[4], acc_o[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  ar_layer(r.tiles + T.f1, sb, img[1], lane, w, acc);
-  ar_epi(acc, tab, img[0], w, lane);  // h1
+  for (int i = 0; i < 4; ++i) acc[i] = acc_o[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  ar_layer(r.tiles + T.f1, sb, img[1], lane, w, acc, acc_o);
+  ar_epi(acc, acc_o, tab, img[0], w, lane);  // h1
   __syncthreads();
-  ar_layer(r.tiles + T.f2, hb, img[0], lane, w, acc);
-  ar_epi(acc, tab + 256, img[1], w, lane);  // h2
+  ar_layer(r.tiles + T.f2, hb, img[0], lane, w, acc, acc_o);
+  ar_epi(acc, acc_o, tab + 256, img[1], w, lane);  // h2
   __syncthreads();
-  ar_layer(r.tiles + T.fa, hb, img[1], lane, w, acc);
-  ar_epi(acc, tab + 512, img[0], w, lane);  // a1
-  ar_layer(r.tiles + T.fc, hb, img[1], lane, w, acc);
-  ar_epi(acc, tab + 768, img[2], w, lane);  // c1
+  ar_layer(r.tiles + T.fa, hb, img[1], lane, w, acc, acc_o);
+  ar_epi(acc, acc_o, tab + 512, img[0], w, lane);  // a1
+  ar_layer(r.tiles + T.fc, hb, img[1], lane, w, acc, acc_o);
+  ar_epi(acc, acc_o, tab + 768, img[2], w, lane);  // c1
   __syncthreads();
   if (w != 0) return;
-  // the head: ppo_rows_r's dot products (same order), then act()'s sample of row c
+  // the head: the step's dot products (same order: ppo_rows_k sums each parity of the output
+  // tiles, lane-reduced, then the two), then act()'s sample of row c
   float p0 = 0.0f, p1 = 0.0f, pv = 0.0f;
+  {
+    constexpr int NP = HWY_ROWS_R == 2 ? 2 : 1;  // parities summed separately
+    float pp[NP][3];
 #pragma unroll
-  for (int nb = 0; nb < 16; ++nb) {
-    const f32x4 a1 = img[0][nb * 64 + lane], c1 = img[2][nb * 64 + lane];
-    const f32x4 x0 = *reinterpret_cast<const f32x4*>(tab + 1024 + 16 * nb + 4 * g);
-    const f32x4 x1 = *reinterpret_cast<const f32x4*>(tab + 1280 + 16 * nb + 4 * g);
-    const f32x4 xc = *reinterpret_cast<const f32x4*>(tab + 1536 + 16 * nb + 4 * g);
+    for (int hp = 0; hp < NP; ++hp) {
+      float s0 = 0.0f, s1 = 0.0f, sv = 0.0f;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      p0 += a1[q] * x0[q];
-      p1 += a1[q] * x1[q];
-      pv += c1[q] * xc[q];
+      for (int i = 0; i < 16 / NP; ++i) {
+        const int nb = NP * i + hp;
+        const f32x4 a1 = img[0][nb * 64 + lane], c1 = img[2][nb * 64 + lane];
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(tab + 1024 + 16 * nb + 4 * g);
+        const f32x4 x1 = *reinterpret_cast<const f32x4*>(tab + 1280 + 16 * nb + 4 * g);
+        const f32x4 xc = *reinterpret_cast<const f32x4*>(tab + 1536 + 16 * nb + 4 * g);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          s0 += a1[q] * x0[q];
+          s1 += a1[q] * x1[q];
+          sv += c1[q] * xc[q];
+        }
+      }
+      s0 += __shfl_xor(s0, 16), s1 += __shfl_xor(s1, 16), sv += __shfl_xor(sv, 16);
+      s0 += __shfl_xor(s0, 32), s1 += __shfl_xor(s1, 32), sv += __shfl_xor(sv, 32);
+      pp[hp][0] = s0, pp[hp][1] = s1, pp[hp][2] = sv;
     }
+    p0 = pp[0][0], p1 = pp[0][1], pv = pp[0][2];
+    if (NP == 2) p0 = p0 + pp[NP - 1][0], p1 = p1 + pp[NP - 1][1], pv = pv + pp[NP - 1][2];
   }
-  p0 += __shfl_xor(p0, 16), p1 += __shfl_xor(p1, 16), pv += __shfl_xor(pv, 16);
-  p0 += __shfl_xor(p0, 32), p1 += __shfl_xor(p1, 32), pv += __shfl_xor(pv, 32);
   if (g != 0 || c >= nrows) return;
   const long b = row0 + c;
   const float ba0 = P[r.off[P_BA2]], ba1 = P[r.off[P_BA2] + 1], bcv = P[r.off[P_BC2]];
@@ -3392,7 +3799,15 @@ static int fused_rows_wgrad(const hwy_ppo_args* a, const Work& w, const Layout& 
   r.counters = a->counters;
   // 8 waves (2 per SIMD) when the columns split into 16-wide tiles, else 4
   const dim3 g1(w.n1), b4(256), b8(512);
-  if (w.rt == 4 * kRowTile && HWY_ROWS_R) {
+  if (w.rt == 4 * kRowTile && HWY_ROWS_R == 2) {
+    const dim3 bk(64 * kRkWaves);
+    switch (w.sb) {
+      case 4: hipLaunchKernelGGL((ppo_rows_k<4>), g1, bk, 0, s, r); break;
+      case 8: hipLaunchKernelGGL((ppo_rows_k<8>), g1, bk, 0, s, r); break;
+      case 12: hipLaunchKernelGGL((ppo_rows_k<12>), g1, bk, 0, s, r); break;
+      default: hipLaunchKernelGGL((ppo_rows_k<16>), g1, bk, 0, s, r); break;
+    }
+  } else if (w.rt == 4 * kRowTile && HWY_ROWS_R == 1) {
     const dim3 br(64 * kRrWaves);
     switch (w.sb) {
       case 4: hipLaunchKernelGGL((ppo_rows_r<4>), g1, br, 0, s, r); break;
@@ -3701,7 +4116,7 @@ int hwy_ppo_act(const hwy_ppo_act_args* a, void* stream) {
   };
   // H = 256 from the tile image: the compact kernel, 32-row tiles once there are two per CU
   // (16,384 rows on MI355X: 91.3 -> 69.4 us), else 16-row tiles (4,096 rows: 25.1 -> 22.0 us)
-  if (HWY_ROWS_R && r.tiles && d.H == 256 && a->learner_rows > 0 &&
+  if (HWY_ROWS_R > 0 && r.tiles && d.H == 256 && a->learner_rows > 0 &&
       rows_tile(a->learner_rows, d.H) == 4 * kRowTile) {
     // the learner's minibatch step runs ppo_rows_r: act with its forward bits
     hipLaunchKernelGGL(ppo_act_r, dim3((d.B + 15) / 16), dim3(256), 0, s, r);

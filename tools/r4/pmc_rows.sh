@@ -3,7 +3,7 @@
 # libhwy_c64.so) at the bench minibatch; the instruction-cache pass is allowed to fail.
 R=$(pwd); H=$R/highway-rope-ppo_amd/hwy; O=$R/gpurun_out/pmcr; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-for lib in libhwy.so libhwy_c64.so; do
+for lib in libhwy_roll.so libhwy.so libhwy_c64.so; do
   i=0
   for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE" \
              "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_WAVES" \
@@ -17,10 +17,11 @@ done
 O=$O python3 - <<'PY'
 import csv, glob, collections, os
 O = os.environ.get("O", "gpurun_out/pmcr")
-for lib in ("libhwy", "libhwy_c64"):
+for lib in ("libhwy_roll", "libhwy", "libhwy_c64"):
     tot = collections.defaultdict(float); n = collections.defaultdict(int)
     for f in glob.glob(f"{O}/{lib}_*/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             tot[r["Counter_Name"]] += float(r["Counter_Value"]); n[r["Counter_Name"]] += 1
     print(lib, {k: f"{v:.4g}" for k, v in sorted(tot.items())})
 PY
+cd $R && bash tools/r4/ab_rows_r2.sh
