@@ -118,11 +118,6 @@ constexpr int kMaxRowS = 256;  // states dim bound of the fused path (LDS)
 #ifndef HWY_WG_DMA
 #define HWY_WG_DMA 1  // ppo_wgrad stages its chunks by LDS-DMA (wgrad_tile_dma); 0: register staging
 #endif
-#ifndef HWY_ROWS_R
-// 64-row tiles at H = 256: 2 ppo_rows_k (activations in registers, split-K wave pairs), 1 ppo_rows_r
-// (activations in registers, one wave per SIMD), 0 ppo_rows_c64
-#define HWY_ROWS_R 2
-#endif
 #ifndef HWY_ROWS_C64
 #define HWY_ROWS_C64 1  // 64-row ppo_rows_c tiles at H = 256 (one workgroup per CU); 0: 32-row tiles
 #endif
@@ -479,7 +474,6 @@ inline int chunk_for(int K, int split) {
   return (c + kKStep - 1) / kKStep * kKStep;
 }
 
-constexpr int kBarF = 320;  // ppo_wsum_adam's barrier words (10 lines of 128 B), the workspace's last
 struct Work {
   float *h1, *h2, *ac, *dac, *dh2, *dh1;
   float *head_part;   // [max(nhead, 4 * n1)][HP]
@@ -490,7 +484,6 @@ struct Work {
   float *wg_slab;            // fused: [ntile][split][kWgPart] partial tiles
   float *xg;                 // fused: [B][S] gathered states
   float *wtile;              // fused: weight tile image (TileGeom)
-  uint32_t *bar;             // fused: ppo_wsum_adam's grid-barrier words (zeroed by sync_params)
   int nhead, HP, sa, s2, s1, ca, c2, c1, nred;
   // fused path (ppo_rows + ppo_wgrad)
   bool fused;
@@ -651,23 +644,21 @@ inline Work carve(const hwy_ppo_dims& d, void* ws, int64_t* bytes_out) {
   const int64_t xg_n = w.fused ? (int64_t)B * S : 0;
   rows_blocks(S, H, &w.sb, &w.hb);
   const int64_t tile_n = w.fused ? tile_geom(S, H, w.sb, w.hb).total : 0;
-  int64_t sizes[18] = {
+  int64_t sizes[17] = {
       (int64_t)B * H, (int64_t)B * H, (int64_t)B * 2 * H, (int64_t)B * 2 * H, (int64_t)B * H,
       (int64_t)B * H, head_rows * w.HP, sa * 2 * H * H, sa * 2 * H,
       s2 * H * H, s2 * H, s1 * H * S, s1 * H,
-      norm_n, wg_slab_n, xg_n, tile_n, w.fused ? kBarF : 0};
+      norm_n, wg_slab_n, xg_n, tile_n};
   float* p = (float*)ws;
-  float* bar = nullptr;
-  float** dst[18] = {&w.h1, &w.h2, &w.ac, &w.dac, &w.dh2, &w.dh1, &w.head_part, &w.slab_ac,
+  float** dst[17] = {&w.h1, &w.h2, &w.ac, &w.dac, &w.dh2, &w.dh1, &w.head_part, &w.slab_ac,
                      &w.bias_ac, &w.slab_2, &w.bias_2, &w.slab_1, &w.bias_1, &w.norm_part,
-                     &w.wg_slab, &w.xg, &w.wtile, &bar};
+                     &w.wg_slab, &w.xg, &w.wtile};
   int64_t total = 0;
-  for (int i = 0; i < 18; ++i) {
+  for (int i = 0; i < 17; ++i) {
     int64_t n = (sizes[i] + 63) / 64 * 64;  // 256-B aligned sub-buffers
     if (p) *dst[i] = p + total;
     total += n;
   }
-  w.bar = (uint32_t*)bar;
   if (bytes_out) *bytes_out = total * (int64_t)sizeof(float);
   return w;
 }
@@ -1696,972 +1687,6 @@ ppo_act_c(ActArgs r) {
   r.value[b] = val;
 }
 
-// ----------------------------------------------------------------------------- ppo_rows_r
-// The row kernel with the activations in registers (H = 256, 64-row tiles: 4 waves, one per
-// SIMD, 16 minibatch rows each).  Every layer runs transposed, out^T = W in^T: the weights are
-// the MFMA's A operand -- the tile image's fragments as they are (lane (g, c) of tile (nb, kb)
-// holds W[16 nb + c][16 kb + 4 g + j], j = 0..3) -- and the activations the B operand.  The C
-// layout of a layer's output, lane (g, c) holding out[row c][16 nb + 4 g + r] for r = 0..3, is
-// then exactly the B operand of the next layer at k-block nb, k-step r: activations never leave
-// the registers.  No LDS images, no epilogue barriers, no LDS copy-out passes; the loss head of a
-// wave's 16 rows runs inside the wave (16-lane DPP sums), and its dL/d[a1|c1] is the B operand of
-// dh2 as computed.  The weights stream once per workgroup through an LDS ring, by LDS-DMA (a slot
-// = 2 k-blocks x the 16 output tiles, 32 KB; each wave DMAs a quarter), shared by the 4 waves:
-// one raw barrier per slot, counted vmcnt waits, 3 slots in flight.  The activations ppo_wgrad
-// reads go to HBM from the registers (16-B stores, 16 rows x 64 B per instruction).
-constexpr int kRrWaves = 4;                     // one wave per SIMD
-constexpr int kRrRows = 16 * kRrWaves;          // minibatch rows per workgroup
-constexpr int kRrRing = 4;                      // ring slots
-constexpr int kRrSlotF = 2 * 16 * 256;          // floats per slot: 2 k-blocks x 16 tiles of 1 KB
-constexpr int kRrDma = 2 * 16 / kRrWaves;       // LDS-DMA instructions per wave and slot
-// LDS (floats): the ring | b1, b2, ba1, bc1 | wa2 row 0, wa2 row 1, wc2 | the head combine (per
-// wave: 3 x 256 head-weight gradient sums, 16 tail sums)
-constexpr int kRrLdsBias = kRrRing * kRrSlotF;
-constexpr int kRrLdsHw = kRrLdsBias + 4 * 256;
-constexpr int kRrLdsComb = kRrLdsHw + 3 * 256;
-constexpr int kRrComb = 3 * 256 + 16;
-constexpr int kRrLdsF = kRrLdsComb + kRrWaves * kRrComb;
-static_assert(kRrLdsF * 4 <= 160 * 1024, "ppo_rows_r LDS");
-
-typedef __attribute__((address_space(3))) void lds_void_t;
-
-template <int I, int N, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<I + 1, N>(f);
-  }
-}
-
-// The stream of ring slots: W1 (SB k-blocks) first, then the six 16-k-block segments in tile-image
-// order f2, fa, fc (forward), ba, bc, b2 (backward).  Tile (nb, kb) of slot q's k-block kbl.
-template <int SB>
-__device__ __forceinline__ const float* rr_tile(const float* tiles, int q, int kbl, int nb) {
-  constexpr int Q1 = SB / 2;
-  if (q < Q1) return tiles + ((long)nb * SB + 2 * q + kbl) * 256;
-  const int s = (q - Q1) / 8, kb = 2 * ((q - Q1) % 8) + kbl;
-  return tiles + ((long)16 * SB + (long)s * 256 + nb * 16 + kb) * 256;
-}
-
-// this wave's quarter of slot q: output tiles 4 w .. 4 w + 3 of both k-blocks (1 KB each)
-template <int SB>
-__device__ __forceinline__ void rr_dma(float* lds, const float* tiles, int q, int w, int lane) {
-  float* slot = lds + (q % kRrRing) * kRrSlotF;
-#pragma unroll
-  for (int i = 0; i < kRrDma; ++i) {
-    const int kbl = i >> 2, nb = 4 * w + (i & 3);
-    __builtin_amdgcn_global_load_lds((const void*)(rr_tile<SB>(tiles, q, kbl, nb) + 4 * lane),
-                                     (lds_void_t*)(slot + (kbl * 16 + nb) * 256), 16, 0, 0);
-  }
-}
-
-// Slot q may be read once this wave's DMAs of it have landed (NY younger slots still in flight:
-// vmcnt counts in issue order, and any younger store only makes the wait stricter) and every
-// other wave's have (the barrier); the barrier also tells the DMA issued next that every wave has
-// finished reading the buffer it overwrites (slot q - 1's).
-template <int NY>
-__device__ __forceinline__ void rr_slot_sync() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NY * kRrDma) : "memory");
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-}
-
-// acc[nb] += W(slot)[nb] x B, k-blocks kbl = 0, 1 with B operands b0, b1 (4 k-steps each).  Eight
-// groups of 4 output tiles; each group's 4 fragment reads go out before the previous group's 16
-// MFMAs (pinned: the scheduler would sink them next to their use and wait for them there)
-__device__ __forceinline__ void rr_mma(const float* slot, int lane, const f32x4& b0,
-                                       const f32x4& b1, f32x4 (&acc)[16]) {
-  const float* base = slot + 4 * lane;
-  f32x4 a[2][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) a[0][i] = *reinterpret_cast<const f32x4*>(base + i * 256);
-#pragma unroll
-  for (int grp = 0; grp < 8; ++grp) {  // grp = 4 kbl + g4: tiles kbl * 16 + 4 g4 + i
-    const int cur = grp & 1;
-    if (grp + 1 < 8) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        a[cur ^ 1][i] = *reinterpret_cast<const f32x4*>(base + (4 * (grp + 1) + i) * 256);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    const f32x4 b = grp < 4 ? b0 : b1;
-    const int g4 = grp & 3;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        acc[4 * g4 + i] =
-            __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][i][j], b[j], acc[4 * g4 + i], 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-// slots Q0 .. Q0 + NQ - 1 of the stream (NS slots in all) into acc, B operands bin[2 s], bin[2 s + 1]
-template <int SB, int NS, int Q0, int NQ, int NIN>
-__device__ __forceinline__ void rr_layer(float* lds, const float* tiles, int w, int lane,
-                                         const f32x4 (&bin)[NIN], f32x4 (&acc)[16]) {
-  static_assert(2 * NQ <= NIN, "B operands of the layer");
-  static_for<0, NQ>([&](auto si) {
-    constexpr int s = decltype(si)::value, q = Q0 + s;
-    constexpr int NY = NS - 1 - q < 2 ? NS - 1 - q : 2;
-    rr_slot_sync<NY>();
-    if constexpr (q + 3 < NS) rr_dma<SB>(lds, tiles, q + 3, w, lane);
-    rr_mma(lds + (q % kRrRing) * kRrSlotF, lane, bin[2 * s], bin[2 * s + 1], acc);
-  });
-}
-
-#ifndef HWY_RR_ROLL
-#define HWY_RR_ROLL 1  // ppo_rows_r's slot loop rolled (2 slots per trip, B operands rotated)
-#endif
-// rr_tile for a run-time slot index
-__device__ __forceinline__ const float* rr_tile_rt(const float* tiles, int SB, int q, int kbl,
-                                                   int nb) {
-  const int Q1 = SB >> 1;
-  if (q < Q1) return tiles + ((long)nb * SB + 2 * q + kbl) * 256;
-  const int s = (q - Q1) >> 3, kb = 2 * ((q - Q1) & 7) + kbl;
-  return tiles + ((long)16 * SB + (long)s * 256 + nb * 16 + kb) * 256;
-}
-
-// one slot at a run-time index q of an NS-slot stream: wait, barrier, the DMA of slot q + 3, the
-// MFMAs (rr_layer's body)
-__device__ __forceinline__ void rr_slot_rt(float* lds, const float* tiles, int SB, int NS, int q,
-                                           int w, int lane, const f32x4& b0, const f32x4& b1,
-                                           f32x4 (&acc)[16]) {
-  if (q + 2 < NS)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kRrDma) : "memory");
-  else if (q + 1 < NS)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRrDma) : "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  if (q + 3 < NS) {
-    const int qn = q + 3;
-    float* slot = lds + (qn & (kRrRing - 1)) * kRrSlotF;
-#pragma unroll
-    for (int i = 0; i < kRrDma; ++i) {
-      const int kbl = i >> 2, nb = 4 * w + (i & 3);
-      __builtin_amdgcn_global_load_lds((const void*)(rr_tile_rt(tiles, SB, qn, kbl, nb) + 4 * lane),
-                                       (lds_void_t*)(slot + (kbl * 16 + nb) * 256), 16, 0, 0);
-    }
-  }
-  rr_mma(lds + (q & (kRrRing - 1)) * kRrSlotF, lane, b0, b1, acc);
-}
-
-// rr_layer as a rolled loop: 2 slots (4 k-blocks) per trip, after which the B operands rotate by
-// 4 (after the last trip they are back in order), so the kernel's code stays a few KB per layer
-template <int NIN>
-__device__ __forceinline__ void rr_layer_rt(float* lds, const float* tiles, int SB, int NS, int Q0,
-                                            int w, int lane, f32x4 (&bin)[NIN], f32x4 (&acc)[16]) {
-  static_assert(NIN % 4 == 0, "whole trips");
-#pragma nounroll
-  for (int it = 0; it < NIN / 4; ++it) {
-    const int q = Q0 + 2 * it;
-    rr_slot_rt(lds, tiles, SB, NS, q, w, lane, bin[0], bin[1], acc);
-    rr_slot_rt(lds, tiles, SB, NS, q + 1, w, lane, bin[2], bin[3], acc);
-    const f32x4 t0 = bin[0], t1 = bin[1], t2 = bin[2], t3 = bin[3];
-#pragma unroll
-    for (int i = 0; i + 4 < NIN; ++i) bin[i] = bin[i + 4];
-    bin[NIN - 4] = t0, bin[NIN - 3] = t1, bin[NIN - 2] = t2, bin[NIN - 1] = t3;
-  }
-}
-
-template <int SB, int NS, int Q0, int NQ, int NIN>
-__device__ __forceinline__ void rr_run(float* lds, const float* tiles, int w, int lane,
-                                       f32x4 (&bin)[NIN], f32x4 (&acc)[16]) {
-  if constexpr (HWY_RR_ROLL && 2 * NQ == NIN)
-    rr_layer_rt<NIN>(lds, tiles, SB, NS, Q0, w, lane, bin, acc);
-  else
-    rr_layer<SB, NS, Q0, NQ>(lds, tiles, w, lane, bin, acc);
-}
-
-// bias + ReLU of a C-layout layer output in place (bias[16 nb + 4 g + r]), its ReLU decisions as
-// bits 4 nb + r
-__device__ __forceinline__ uint64_t rr_bias_relu(f32x4 (&acc)[16], const float* bias, int g) {
-  uint64_t m = 0ull;
-#pragma unroll
-  for (int nb = 0; nb < 16; ++nb) {
-    const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + 16 * nb + 4 * g);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float v = acc[nb][r] + bv[r];
-      v = v > 0.0f ? v : 0.0f;
-      acc[nb][r] = v;
-      m |= (uint64_t)(v > 0.0f ? 1u : 0u) << (4 * nb + r);
-    }
-  }
-  return m;
-}
-
-// the layer's output gradient through the ReLU decisions m (row_epi_maskbits' expression)
-__device__ __forceinline__ void rr_mask(f32x4 (&acc)[16], uint64_t m) {
-#pragma unroll
-  for (int nb = 0; nb < 16; ++nb)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) acc[nb][r] = ((m >> (4 * nb + r)) & 1ull) ? acc[nb][r] : 0.0f;
-}
-
-// a wave's 16 rows of a C-layout H-wide block to HBM (row c at dst + c * ld, live rows only)
-__device__ __forceinline__ void rr_store(float* dst, long ld, bool live, int g, int c,
-                                         const f32x4 (&v)[16]) {
-  if (!live) return;
-  float* p = dst + (long)c * ld + 4 * g;
-#pragma unroll
-  for (int nb = 0; nb < 16; ++nb) *reinterpret_cast<f32x4*>(p + 16 * nb) = v[nb];
-}
-
-template <int SB>
-__global__ void __launch_bounds__(64 * kRrWaves) __attribute__((amdgpu_waves_per_eu(1, 1)))
-ppo_rows_r(RowArgs r) {
-  constexpr int H = 256;
-  constexpr int NS = SB / 2 + 48;  // ring slots of the whole stream
-  constexpr int Q2 = SB / 2, QA = Q2 + 8, QC = QA + 8, QBA = QC + 8, QBC = QBA + 8, QB2 = QBC + 8;
-  __shared__ __attribute__((aligned(16))) float lds[kRrLdsF];
-  CLK_BEGIN
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, g = lane >> 4, c = lane & 15;
-  const int S = r.S;
-  const int row0 = blockIdx.x * kRrRows;
-  const int nrows = min(kRrRows, r.B - row0);
-  const int wr0 = row0 + 16 * w;           // this wave's first row
-  const bool live = 16 * w + c < nrows;    // this lane's row exists
-  const float* P = r.params;
-  const float* tiles = r.tiles;
-  if (blockIdx.x == 0 && t == 0) {
-    r.counters[0] += 1;  // Adam step t for this minibatch
-    r.counters[1] += 1;  // metrics row (this step writes row counters[1]-1)
-  }
-  // ---- plain global loads first, all consumed before the first LDS-DMA (hipcc waits vmcnt(0)
-  // at the use of an ordinary load while an LDS-DMA is in flight)
-  const long src = (long)r.idx[live ? wr0 + c : row0];
-  f32x4 x[SB];  // the states row: B operand of layer 1 (k-block kb, k-steps 4 g + j)
-#pragma unroll
-  for (int kb = 0; kb < SB; ++kb) {
-    const int k = 16 * kb + 4 * g;
-    x[kb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    if (live && k < S) x[kb] = *reinterpret_cast<const f32x4*>(r.states + src * S + k);
-  }
-  const float hz0 = r.pre_tanh[src * 2], hz1 = r.pre_tanh[src * 2 + 1];
-  const float hold = r.old_logp[src], hadv = r.adv[src], hret = r.ret[src];
-  {
-    const int64_t bo[4] = {r.off[P_B1], r.off[P_B2], r.off[P_BA1], r.off[P_BC1]};
-#pragma unroll
-    for (int l = 0; l < 4; ++l) lds[kRrLdsBias + l * 256 + t] = P[bo[l] + t];
-    lds[kRrLdsHw + t] = P[r.off[P_WA2] + t];
-    lds[kRrLdsHw + 256 + t] = P[r.off[P_WA2] + H + t];
-    lds[kRrLdsHw + 512 + t] = P[r.off[P_WC2] + t];
-  }
-  if (live) {
-#pragma unroll
-    for (int kb = 0; kb < SB; ++kb) {
-      const int k = 16 * kb + 4 * g;
-      if (k < S) *reinterpret_cast<f32x4*>(r.xg + (long)(wr0 + c) * S + k) = x[kb];
-    }
-  }
-  const float ba0 = P[r.off[P_BA2]], ba1 = P[r.off[P_BA2] + 1], bcv = P[r.off[P_BC2]];
-  const float ls0 = P[r.off[P_LOGSTD]], ls1 = P[r.off[P_LOGSTD] + 1];
-  // the squash correction of the stored pre-tanh actions, off the head's dependent chain
-  const float hq0 = log1pf(-(tanhf(hz0) * tanhf(hz0)) + 1e-6f);
-  const float hq1 = log1pf(-(tanhf(hz1) * tanhf(hz1)) + 1e-6f);
-  // every ordinary load has returned before the first LDS-DMA goes out
-  asm volatile("" ::"v"(hold), "v"(hadv), "v"(hret), "v"(hq0), "v"(hq1), "v"(ba0), "v"(ba1),
-               "v"(bcv), "v"(ls0), "v"(ls1)
-               : "memory");
-  __syncthreads();  // the bias / head-weight tables (no LDS-DMA in flight yet)
-  rr_dma<SB>(lds, tiles, 0, w, lane);
-  rr_dma<SB>(lds, tiles, 1, w, lane);
-  rr_dma<SB>(lds, tiles, 2, w, lane);
-
-  f32x4 acc[16];
-  // ---- h1 = relu(W1 x + b1)
-#pragma unroll
-  for (int nb = 0; nb < 16; ++nb) acc[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  rr_run<SB, NS, 0, SB / 2>(lds, tiles, w, lane, x, acc);
-  const uint64_t m1 = rr_bias_relu(acc, lds + kRrLdsBias, g);
-  f32x4 h1[16];
-#pragma unroll
-  for (int nb = 0; nb < 16; ++nb) h1[nb] = acc[nb];
-  rr_store(r.h1 + (long)wr0 * H, H, live, g, c, h1);
-  // ---- h2 = relu(W2 h1 + b2)
-#pragma unroll
-  for (int nb = 0; nb < 16; ++nb) acc[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  rr_run<SB, NS, Q2, 8>(lds, tiles, w, lane, h1, acc);
-  const uint64_t m2 = rr_bias_relu(acc, lds + kRrLdsBias + 256, g);
-  f32x4 h2[16];
-#pragma unroll
-  for (int nb = 0; nb < 16; ++nb) h2[nb] = acc[nb];
-  rr_store(r.h2 + (long)wr0 * H, H, live, g, c, h2);
-  // ---- a1 = relu(Wa1 h2 + ba1), c1 = relu(Wc1 h2 + bc1)
-  f32x4 a1[16], c1[16];
-#pragma unroll
-  for (int nb = 0; nb < 16; ++nb) a1[nb] = c1[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  rr_run<SB, NS, QA, 8>(lds, tiles, w, lane, h2, a1);
-  rr_run<SB, NS, QC, 8>(lds, tiles, w, lane, h2, c1);
-  (void)rr_bias_relu(a1, lds + kRrLdsBias + 512, g);
-  (void)rr_bias_relu(c1, lds + kRrLdsBias + 768, g);
-
-  // ---- loss head (ppo/agent.py:226-245) of this wave's 16 rows: mean / value dot products over
-  // the lane's 64 columns, then over the four 16-lane groups (every lane of row c gets its sums)
-  const float* wa0 = lds + kRrLdsHw;
-  const float* wa1 = wa0 + 256;
-  const float* wcv = wa0 + 512;
-  float p0 = 0.0f, p1 = 0.0f, pv = 0.0f;
-#pragma unroll
-  for (int nb = 0; nb < 16; ++nb) {
-    const f32x4 x0 = *reinterpret_cast<const f32x4*>(wa0 + 16 * nb + 4 * g);
-    const f32x4 x1 = *reinterpret_cast<const f32x4*>(wa1 + 16 * nb + 4 * g);
-    const f32x4 xc = *reinterpret_cast<const f32x4*>(wcv + 16 * nb + 4 * g);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      p0 += a1[nb][q] * x0[q];
-      p1 += a1[nb][q] * x1[q];
-      pv += c1[nb][q] * xc[q];
-    }
-  }
-  p0 += __shfl_xor(p0, 16), p1 += __shfl_xor(p1, 16), pv += __shfl_xor(pv, 16);
-  p0 += __shfl_xor(p0, 32), p1 += __shfl_xor(p1, 32), pv += __shfl_xor(pv, 32);
-  float dmu0, dmu1, dv, tl[9];
-  {
-    // torch Normal: scale = exp(log_std); var = scale**2; log_scale = log(scale)
-    const float sc0 = expf(ls0), sc1 = expf(ls1);
-    const float var0 = sc0 * sc0, var1 = sc1 * sc1;
-    const float lsc0 = logf(sc0), lsc1 = logf(sc1);
-    const float LOG_SQRT_2PI = 0.91893853320467274178f;
-    const float invB = 1.0f / (float)r.B;
-    const float lo = 1.0f - r.eps_clip, hi = 1.0f + r.eps_clip;
-    const float mu0 = p0 + ba0, mu1 = p1 + ba1, val = pv + bcv;
-    const float d0 = hz0 - mu0, d1 = hz1 - mu1;
-    const float lp0 = -(d0 * d0) / (2.0f * var0) - lsc0 - LOG_SQRT_2PI;
-    const float lp1 = -(d1 * d1) / (2.0f * var1) - lsc1 - LOG_SQRT_2PI;
-    const float logp = (lp0 - hq0) + (lp1 - hq1);
-    const float log_ratio = logp - hold;
-    const float ratio = expf(log_ratio);
-    const float cr = fminf(fmaxf(ratio, lo), hi);
-    const float s1 = ratio * hadv, s2 = cr * hadv;
-    const float inr = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
-    // torch.min / clamp backward: ties split the gradient evenly
-    const float wsel = s1 < s2 ? 1.0f : (s1 > s2 ? inr : 0.5f * (1.0f + inr));
-    const float dlogp = -invB * hadv * wsel * ratio;  // d(actor_loss)/d(logp)
-    dmu0 = live ? dlogp * d0 / var0 : 0.0f;
-    dmu1 = live ? dlogp * d1 / var1 : 0.0f;
-    dv = live ? r.value_coef * 2.0f * (val - hret) * invB : 0.0f;
-    tl[0] = dmu0, tl[1] = dmu1, tl[2] = dv;
-    tl[3] = live ? dlogp * ((d0 * d0) / var0 - 1.0f) : 0.0f;
-    tl[4] = live ? dlogp * ((d1 * d1) / var1 - 1.0f) : 0.0f;
-    tl[5] = live ? -fminf(s1, s2) : 0.0f;
-    tl[6] = live ? (val - hret) * (val - hret) : 0.0f;
-    tl[7] = live ? (fabsf(ratio - 1.0f) > r.eps_clip ? 1.0f : 0.0f) : 0.0f;
-    tl[8] = live ? (ratio - 1.0f) - log_ratio : 0.0f;
-  }
-  // dL/d[a1 | c1] (the reference's expression per element) becomes dh2's B operand in place; the
-  // head-weight gradients sum_rows dmu a1 / dv c1 of every column over the wave's 16 rows
-  float* comb = lds + kRrLdsComb + w * kRrComb;
-#pragma unroll
-  for (int nb = 0; nb < 16; ++nb) {
-    const f32x4 x0 = *reinterpret_cast<const f32x4*>(wa0 + 16 * nb + 4 * g);
-    const f32x4 x1 = *reinterpret_cast<const f32x4*>(wa1 + 16 * nb + 4 * g);
-    const f32x4 xc = *reinterpret_cast<const f32x4*>(wcv + 16 * nb + 4 * g);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float a = a1[nb][q], cc = c1[nb][q];
-      const float s0 = row16_sum(dmu0 * a), s1 = row16_sum(dmu1 * a), sc = row16_sum(dv * cc);
-      if (c == 0) {
-        const int n = 16 * nb + 4 * g + q;
-        comb[n] = s0;
-        comb[256 + n] = s1;
-        comb[512 + n] = sc;
-      }
-      a1[nb][q] = a > 0.0f ? (dmu0 * x0[q] + dmu1 * x1[q]) : 0.0f;
-      c1[nb][q] = cc > 0.0f ? dv * xc[q] : 0.0f;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    const float v = row16_sum(tl[k]);
-    if (lane == k) comb[768 + k] = v;  // lane k < 16 is in DPP row 0 (g = 0)
-  }
-  rr_store(r.dac + (long)wr0 * 2 * H, 2 * H, live, g, c, a1);
-  rr_store(r.dac + (long)wr0 * 2 * H + H, 2 * H, live, g, c, c1);
-  // the workgroup's head partial row: the four waves' sums in wave order (a raw barrier: the
-  // ring's LDS-DMAs stay in flight)
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  {
-    float* out = r.head_part + (long)blockIdx.x * r.HP;
-    const float* cb = lds + kRrLdsComb;
-    for (int e = t; e < 3 * H + 9; e += 64 * kRrWaves) {
-      float v = cb[e];
-#pragma unroll
-      for (int ww = 1; ww < kRrWaves; ++ww) v += cb[ww * kRrComb + e];
-      out[e] = v;
-    }
-  }
-  // ---- dh2 = (dac [Wa1; Wc1]) * (h2 > 0)
-#pragma unroll
-  for (int nb = 0; nb < 16; ++nb) acc[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  rr_run<SB, NS, QBA, 8>(lds, tiles, w, lane, a1, acc);
-  rr_run<SB, NS, QBC, 8>(lds, tiles, w, lane, c1, acc);
-  rr_mask(acc, m2);
-  f32x4 d2[16];
-#pragma unroll
-  for (int nb = 0; nb < 16; ++nb) d2[nb] = acc[nb];
-  rr_store(r.dh2 + (long)wr0 * H, H, live, g, c, d2);
-  // ---- dh1 = (dh2 W2) * (h1 > 0)
-#pragma unroll
-  for (int nb = 0; nb < 16; ++nb) acc[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  rr_run<SB, NS, QB2, 8>(lds, tiles, w, lane, d2, acc);
-  rr_mask(acc, m1);
-  rr_store(r.dh1 + (long)wr0 * H, H, live, g, c, acc);
-  CLK_END(0);
-}
-
-// ----------------------------------------------------------------------------- ppo_rows_k
-// ppo_rows_r's transposed, register-chained layers at two waves per SIMD (ppo_rows_r's single wave
-// per SIMD left the matrix pipe idle through every wait: MFMA busy 0.58 against ppo_rows_c64's
-// 0.68).  8 waves: wave w owns the 16 rows of row block w & 3 and the k-blocks of parity
-// h = w >> 2 of every layer (split-K; waves w and w + 4 share a SIMD).  Each wave accumulates all 16
-// output tiles over its half of the reduction; at a layer's end the two waves of a row block swap
-// the partial sums of each other's parity through LDS (8 tiles each way) and each finishes the 8
-// output tiles of its own parity -- acc_even + acc_odd, bias, ReLU, stores -- which are exactly its
-// B operands (the k-blocks of its parity) for the next layer.  The loss head's dot products are
-// summed per parity, then added; dL/d[a1|c1] of a wave's own tiles is its B operand for dh2 as
-// computed, so the head needs no tile exchange.  Ring: 2 slots of 2 k-blocks x 16 tiles (each wave
-// reads the k-block of its parity, DMAs 4 tiles), one barrier per slot; a layer boundary's
-// exchange, epilogue and stores run after the next slot's barrier, before that slot's DMA.
-constexpr int kRkWaves = 8;
-constexpr int kRkRows = 64;
-constexpr int kRkDma = 2 * 16 / kRkWaves;
-// LDS (floats): ring (2 slots) | exchange [8 waves][8 tiles][64 lanes] f32x4 | b1 b2 ba1 bc1 |
-// wa2 row 0, row 1, wc2 | head dot-product exchange [8 waves][16 rows] f32x4 | head combine
-// [8 waves][3 x 128 column sums + 16 tail sums]
-constexpr int kRkLdsX = 2 * kRrSlotF;
-constexpr int kRkLdsBias = kRkLdsX + kRkWaves * 8 * 64 * 4;
-constexpr int kRkLdsHw = kRkLdsBias + 4 * 256;
-constexpr int kRkLdsP = kRkLdsHw + 3 * 256;
-constexpr int kRkComb = 3 * 128 + 16;
-constexpr int kRkLdsComb = kRkLdsP + kRkWaves * 16 * 4;
-constexpr int kRkLdsF = kRkLdsComb + kRkWaves * kRkComb;
-static_assert(kRkLdsF * 4 <= 160 * 1024, "ppo_rows_k LDS");
-
-// this wave's 4 tiles of slot q: k-block h of the slot, output tiles 4 (w & 3) .. + 3
-template <int SB>
-__device__ __forceinline__ void rk_dma(float* lds, const float* tiles, int q, int w, int lane) {
-  float* slot = lds + (q & 1) * kRrSlotF;
-  const int kbl = w >> 2;
-#pragma unroll
-  for (int i = 0; i < kRkDma; ++i) {
-    const int nb = 4 * (w & 3) + i;
-    __builtin_amdgcn_global_load_lds((const void*)(rr_tile<SB>(tiles, q, kbl, nb) + 4 * lane),
-                                     (lds_void_t*)(slot + (kbl * 16 + nb) * 256), 16, 0, 0);
-  }
-}
-
-// acc[nb] += W(k-block tiles)[nb] x b over one k-block (16 tiles at kt, 4 groups of 4, each
-// group's fragment reads issued before the previous group's MFMAs)
-__device__ __forceinline__ void rk_mma(const float* kt, int lane, const f32x4& b,
-                                       f32x4 (&acc)[16]) {
-  const float* base = kt + 4 * lane;
-  f32x4 a[2][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) a[0][i] = *reinterpret_cast<const f32x4*>(base + i * 256);
-#pragma unroll
-  for (int g4 = 0; g4 < 4; ++g4) {
-    const int cur = g4 & 1;
-    if (g4 + 1 < 4) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        a[cur ^ 1][i] = *reinterpret_cast<const f32x4*>(base + (4 * (g4 + 1) + i) * 256);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        acc[4 * g4 + i] =
-            __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][i][j], b[j], acc[4 * g4 + i], 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-// slot Q: its DMAs (issued one slot ago) landed for every wave (nothing younger is in flight: the
-// stores of a layer boundary go out before the next DMA), then `pre` (a layer boundary's work),
-// then the DMA of slot Q + 1 into the other buffer, then this wave's MFMAs
-template <int SB, int NS, int Q, class PRE>
-__device__ __forceinline__ void rk_slot(float* lds, const float* tiles, int w, int lane,
-                                        const f32x4& b, f32x4 (&acc)[16], PRE&& pre) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  pre();
-  if constexpr (Q + 1 < NS) rk_dma<SB>(lds, tiles, Q + 1, w, lane);
-  rk_mma(lds + (Q & 1) * kRrSlotF + (w >> 2) * 16 * 256, lane, b, acc);
-}
-
-// slots Q0 .. Q0 + NQ - 1 with this wave's B operands bh[s]; `pre` runs in the first slot
-template <int SB, int NS, int Q0, int NQ, class PRE>
-__device__ __forceinline__ void rk_layer(float* lds, const float* tiles, int w, int lane,
-                                         const f32x4 (&bh)[NQ], f32x4 (&acc)[16], PRE&& pre) {
-  static_for<0, NQ>([&](auto si) {
-    constexpr int s = decltype(si)::value;
-    if constexpr (s == 0)
-      rk_slot<SB, NS, Q0 + s>(lds, tiles, w, lane, bh[s], acc, pre);
-    else
-      rk_slot<SB, NS, Q0 + s>(lds, tiles, w, lane, bh[s], acc, [] {});
-  });
-}
-
-// the partner's (other parity) half of a layer boundary: this wave's partial sums of the tiles of
-// the other parity into the exchange image
-__device__ __forceinline__ void rk_put(float* lds, int w, int lane, const f32x4 (&acc)[16]) {
-  f32x4* X = reinterpret_cast<f32x4*>(lds + kRkLdsX) + w * 8 * 64;
-  const bool odd = (w >> 2) == 0;  // the partner's parity (a select: no run-time register index)
-#pragma unroll
-  for (int i = 0; i < 8; ++i) X[i * 64 + lane] = odd ? acc[2 * i + 1] : acc[2 * i];
-}
-// this wave's own tiles (2 i + h): its partial + the partner's
-__device__ __forceinline__ void rk_get(const float* lds, int w, int lane, const f32x4 (&acc)[16],
-                                       f32x4 (&out)[8]) {
-  const f32x4* X = reinterpret_cast<const f32x4*>(lds + kRkLdsX) + (w ^ 4) * 8 * 64;
-  const bool odd = (w >> 2) != 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) out[i] = (odd ? acc[2 * i + 1] : acc[2 * i]) + X[i * 64 + lane];
-}
-// bias + ReLU of the own tiles (nb = 2 i + h), their ReLU decisions as bits 4 i + r
-__device__ __forceinline__ uint32_t rk_bias_relu(f32x4 (&v)[8], const float* bias, int h, int g) {
-  uint32_t m = 0u;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + 16 * (2 * i + h) + 4 * g);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float x = v[i][r] + bv[r];
-      x = x > 0.0f ? x : 0.0f;
-      v[i][r] = x;
-      m |= (x > 0.0f ? 1u : 0u) << (4 * i + r);
-    }
-  }
-  return m;
-}
-__device__ __forceinline__ void rk_mask(f32x4 (&v)[8], uint32_t m) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[i][r] = ((m >> (4 * i + r)) & 1u) ? v[i][r] : 0.0f;
-}
-__device__ __forceinline__ void rk_store(float* dst, long ld, bool live, int h, int g, int c,
-                                         const f32x4 (&v)[8]) {
-  if (!live) return;
-  float* p = dst + (long)c * ld + 4 * g;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) *reinterpret_cast<f32x4*>(p + 16 * (2 * i + h)) = v[i];
-}
-__device__ __forceinline__ void rk_zero(f32x4 (&acc)[16]) {
-#pragma unroll
-  for (int nb = 0; nb < 16; ++nb) acc[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-}
-
-template <int SB>
-__global__ void __launch_bounds__(64 * kRkWaves) __attribute__((amdgpu_waves_per_eu(2, 2)))
-ppo_rows_k(RowArgs r) {
-  constexpr int H = 256;
-  constexpr int NS = SB / 2 + 48;
-  constexpr int Q2 = SB / 2, QA = Q2 + 8, QC = QA + 8, QBA = QC + 8, QBC = QBA + 8, QB2 = QBC + 8;
-  __shared__ __attribute__((aligned(16))) float lds[kRkLdsF];
-  CLK_BEGIN
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, g = lane >> 4, c = lane & 15;
-  const int rb = w & 3, h = w >> 2;
-  const int S = r.S;
-  const int row0 = blockIdx.x * kRkRows;
-  const int nrows = min(kRkRows, r.B - row0);
-  const int wr0 = row0 + 16 * rb;           // this wave's first row
-  const bool live = 16 * rb + c < nrows;    // this lane's row exists
-  const float* P = r.params;
-  const float* tiles = r.tiles;
-  if (blockIdx.x == 0 && t == 0) {
-    r.counters[0] += 1;  // Adam step t for this minibatch
-    r.counters[1] += 1;  // metrics row (this step writes row counters[1]-1)
-  }
-  // ---- plain global loads first, all consumed before the first LDS-DMA (hipcc waits vmcnt(0)
-  // at the use of an ordinary load while an LDS-DMA is in flight)
-  const long src = (long)r.idx[live ? wr0 + c : row0];
-  f32x4 x[SB / 2];  // layer 1's B operands: the states row's k-blocks 2 i + h
-#pragma unroll
-  for (int i = 0; i < SB / 2; ++i) {
-    const int k = 16 * (2 * i + h) + 4 * g;
-    x[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    if (live && k < S) x[i] = *reinterpret_cast<const f32x4*>(r.states + src * S + k);
-  }
-  const float hz0 = r.pre_tanh[src * 2], hz1 = r.pre_tanh[src * 2 + 1];
-  const float hold = r.old_logp[src], hadv = r.adv[src], hret = r.ret[src];
-  for (int e = t; e < 4 * 256; e += 64 * kRkWaves) {
-    const int l = e >> 8, n = e & 255;
-    const int64_t bo = l == 0 ? r.off[P_B1] : l == 1 ? r.off[P_B2] : l == 2 ? r.off[P_BA1] : r.off[P_BC1];
-    lds[kRkLdsBias + e] = P[bo + n];
-  }
-  for (int e = t; e < 3 * 256; e += 64 * kRkWaves) {
-    const int l = e >> 8, n = e & 255;
-    lds[kRkLdsHw + e] = P[(l == 2 ? r.off[P_WC2] : r.off[P_WA2] + l * H) + n];
-  }
-  if (live) {
-#pragma unroll
-    for (int i = 0; i < SB / 2; ++i) {
-      const int k = 16 * (2 * i + h) + 4 * g;
-      if (k < S) *reinterpret_cast<f32x4*>(r.xg + (long)(wr0 + c) * S + k) = x[i];
-    }
-  }
-  const float ba0 = P[r.off[P_BA2]], ba1 = P[r.off[P_BA2] + 1], bcv = P[r.off[P_BC2]];
-  const float ls0 = P[r.off[P_LOGSTD]], ls1 = P[r.off[P_LOGSTD] + 1];
-  // the squash correction of the stored pre-tanh actions, off the head's dependent chain
-  const float hq0 = log1pf(-(tanhf(hz0) * tanhf(hz0)) + 1e-6f);
-  const float hq1 = log1pf(-(tanhf(hz1) * tanhf(hz1)) + 1e-6f);
-  // every ordinary load has returned before the first LDS-DMA goes out
-  asm volatile("" ::"v"(hold), "v"(hadv), "v"(hret), "v"(hq0), "v"(hq1), "v"(ba0), "v"(ba1),
-               "v"(bcv), "v"(ls0), "v"(ls1)
-               : "memory");
-  __syncthreads();  // the bias / head-weight tables (no LDS-DMA in flight yet)
-  rk_dma<SB>(lds, tiles, 0, w, lane);
-  const float* bias = lds + kRkLdsBias;
-
-  f32x4 acc[16];
-  f32x4 v1[8], v2[8], a1[8], c1[8];
-  uint32_t m1 = 0u, m2 = 0u;
-  // ---- h1 = relu(W1 x + b1)
-  rk_zero(acc);
-  rk_layer<SB, NS, 0, SB / 2>(lds, tiles, w, lane, x, acc, [] {});
-  rk_put(lds, w, lane, acc);
-  // ---- h2 = relu(W2 h1 + b2); the boundary (h1's exchange, epilogue, stores) in its first slot
-  {
-    f32x4 acc2[16];
-    rk_zero(acc2);
-    rk_layer<SB, NS, Q2, 8>(lds, tiles, w, lane, v1, acc2, [&] {
-      rk_get(lds, w, lane, acc, v1);
-      m1 = rk_bias_relu(v1, bias, h, g);
-      rk_store(r.h1 + (long)wr0 * H, H, live, h, g, c, v1);
-    });
-    rk_put(lds, w, lane, acc2);
-#pragma unroll
-    for (int nb = 0; nb < 16; ++nb) acc[nb] = acc2[nb];
-  }
-  // ---- a1 = relu(Wa1 h2 + ba1), c1 = relu(Wc1 h2 + bc1)
-  {
-    f32x4 acc2[16];
-    rk_zero(acc2);
-    rk_layer<SB, NS, QA, 8>(lds, tiles, w, lane, v2, acc2, [&] {
-      rk_get(lds, w, lane, acc, v2);
-      m2 = rk_bias_relu(v2, bias + 256, h, g);
-      rk_store(r.h2 + (long)wr0 * H, H, live, h, g, c, v2);
-    });
-    rk_put(lds, w, lane, acc2);
-    rk_zero(acc);
-    rk_layer<SB, NS, QC, 8>(lds, tiles, w, lane, v2, acc, [&] {
-      rk_get(lds, w, lane, acc2, a1);
-      (void)rk_bias_relu(a1, bias + 512, h, g);
-    });
-    rk_put(lds, w, lane, acc);
-  }
-  // ---- loss head (ppo/agent.py:226-245), at the first dh2 slot's boundary: c1's exchange, the
-  // dot products per parity (then the pair's sum), the per-row scalars, dL/d[a1 | c1] of the own
-  // tiles (dh2's B operands), the head-weight gradient column sums into the combine image
-  const float* wa0 = lds + kRkLdsHw;
-  const float* wa1 = wa0 + 256;
-  const float* wcv = wa0 + 512;
-  float tl[9];
-  auto head = [&] {
-    rk_get(lds, w, lane, acc, c1);
-    (void)rk_bias_relu(c1, bias + 768, h, g);
-    float p0 = 0.0f, p1 = 0.0f, pv = 0.0f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int o = 16 * (2 * i + h) + 4 * g;
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(wa0 + o);
-      const f32x4 x1 = *reinterpret_cast<const f32x4*>(wa1 + o);
-      const f32x4 xc = *reinterpret_cast<const f32x4*>(wcv + o);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        p0 += a1[i][q] * x0[q];
-        p1 += a1[i][q] * x1[q];
-        pv += c1[i][q] * xc[q];
-      }
-    }
-    p0 += __shfl_xor(p0, 16), p1 += __shfl_xor(p1, 16), pv += __shfl_xor(pv, 16);
-    p0 += __shfl_xor(p0, 32), p1 += __shfl_xor(p1, 32), pv += __shfl_xor(pv, 32);
-    f32x4* PX = reinterpret_cast<f32x4*>(lds + kRkLdsP);
-    if (g == 0) PX[w * 16 + c] = f32x4{p0, p1, pv, 0.0f};
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    const f32x4 po = PX[(w ^ 4) * 16 + c];
-    p0 = p0 + po[0], p1 = p1 + po[1], pv = pv + po[2];  // the even + odd parity sums (commutative)
-    // torch Normal: scale = exp(log_std); var = scale**2; log_scale = log(scale)
-    const float sc0 = expf(ls0), sc1 = expf(ls1);
-    const float var0 = sc0 * sc0, var1 = sc1 * sc1;
-    const float lsc0 = logf(sc0), lsc1 = logf(sc1);
-    const float LOG_SQRT_2PI = 0.91893853320467274178f;
-    const float invB = 1.0f / (float)r.B;
-    const float lo = 1.0f - r.eps_clip, hi = 1.0f + r.eps_clip;
-    const float mu0 = p0 + ba0, mu1 = p1 + ba1, val = pv + bcv;
-    const float d0 = hz0 - mu0, d1 = hz1 - mu1;
-    const float lp0 = -(d0 * d0) / (2.0f * var0) - lsc0 - LOG_SQRT_2PI;
-    const float lp1 = -(d1 * d1) / (2.0f * var1) - lsc1 - LOG_SQRT_2PI;
-    const float logp = (lp0 - hq0) + (lp1 - hq1);
-    const float log_ratio = logp - hold;
-    const float ratio = expf(log_ratio);
-    const float cr = fminf(fmaxf(ratio, lo), hi);
-    const float s1 = ratio * hadv, s2 = cr * hadv;
-    const float inr = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
-    // torch.min / clamp backward: ties split the gradient evenly
-    const float wsel = s1 < s2 ? 1.0f : (s1 > s2 ? inr : 0.5f * (1.0f + inr));
-    const float dlogp = -invB * hadv * wsel * ratio;  // d(actor_loss)/d(logp)
-    const float dmu0 = live ? dlogp * d0 / var0 : 0.0f;
-    const float dmu1 = live ? dlogp * d1 / var1 : 0.0f;
-    const float dv = live ? r.value_coef * 2.0f * (val - hret) * invB : 0.0f;
-    tl[0] = dmu0, tl[1] = dmu1, tl[2] = dv;
-    tl[3] = live ? dlogp * ((d0 * d0) / var0 - 1.0f) : 0.0f;
-    tl[4] = live ? dlogp * ((d1 * d1) / var1 - 1.0f) : 0.0f;
-    tl[5] = live ? -fminf(s1, s2) : 0.0f;
-    tl[6] = live ? (val - hret) * (val - hret) : 0.0f;
-    tl[7] = live ? (fabsf(ratio - 1.0f) > r.eps_clip ? 1.0f : 0.0f) : 0.0f;
-    tl[8] = live ? (ratio - 1.0f) - log_ratio : 0.0f;
-    float* comb = lds + kRkLdsComb + w * kRkComb;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int o = 16 * (2 * i + h) + 4 * g;
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(wa0 + o);
-      const f32x4 x1 = *reinterpret_cast<const f32x4*>(wa1 + o);
-      const f32x4 xc = *reinterpret_cast<const f32x4*>(wcv + o);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float a = a1[i][q], cc = c1[i][q];
-        const float s0 = row16_sum(dmu0 * a), s1v = row16_sum(dmu1 * a), sc = row16_sum(dv * cc);
-        if (c == 0) {
-          const int nl = 16 * i + 4 * g + q;  // column 16 (2 i + h) + 4 g + q among this parity's
-          comb[nl] = s0;
-          comb[128 + nl] = s1v;
-          comb[256 + nl] = sc;
-        }
-        a1[i][q] = a > 0.0f ? (dmu0 * x0[q] + dmu1 * x1[q]) : 0.0f;
-        c1[i][q] = cc > 0.0f ? dv * xc[q] : 0.0f;
-      }
-    }
-    if (h == 0) {  // the row scalars once per row block (both waves of a pair hold them)
-#pragma unroll
-      for (int k = 0; k < 9; ++k) {
-        const float v = row16_sum(tl[k]);
-        if (lane == k) comb[384 + k] = v;  // lane k < 16 is in DPP row 0 (g = 0)
-      }
-    }
-    rk_store(r.dac + (long)wr0 * 2 * H, 2 * H, live, h, g, c, a1);
-    rk_store(r.dac + (long)wr0 * 2 * H + H, 2 * H, live, h, g, c, c1);
-  };
-  // ---- dh2 = (dac [Wa1; Wc1]) * (h2 > 0); the head partial row of the workgroup (the combine
-  // image complete behind the second dh2 slot's barrier) in that slot
-  {
-    f32x4 acc2[16];
-    rk_zero(acc2);
-    static_for<0, 8>([&](auto si) {
-      constexpr int s = decltype(si)::value;
-      if constexpr (s == 0) {
-        rk_slot<SB, NS, QBA>(lds, tiles, w, lane, a1[0], acc2, head);
-      } else if constexpr (s == 1) {
-        rk_slot<SB, NS, QBA + 1>(lds, tiles, w, lane, a1[1], acc2, [&] {
-          float* out = r.head_part + (long)blockIdx.x * r.HP;
-          const float* cb = lds + kRkLdsComb;
-          for (int e = t; e < 3 * H + 9; e += 64 * kRkWaves) {
-            int hh = 0, o;
-            if (e < 3 * H) {
-              const int k = e >> 8, n = e & 255;
-              hh = (n >> 4) & 1;
-              o = 128 * k + 16 * (n >> 5) + (n & 15);
-            } else {
-              o = 384 + (e - 3 * H);
-            }
-            float v = cb[(4 * hh) * kRkComb + o];
-#pragma unroll
-            for (int q = 1; q < 4; ++q) v += cb[(q + 4 * hh) * kRkComb + o];
-            out[e] = v;
-          }
-        });
-      } else {
-        rk_slot<SB, NS, QBA + s>(lds, tiles, w, lane, a1[s], acc2, [] {});
-      }
-    });
-    rk_layer<SB, NS, QBC, 8>(lds, tiles, w, lane, c1, acc2, [] {});
-    rk_put(lds, w, lane, acc2);
-    // ---- dh1 = (dh2 W2) * (h1 > 0)
-    rk_zero(acc);
-    rk_layer<SB, NS, QB2, 8>(lds, tiles, w, lane, v2, acc, [&] {
-      rk_get(lds, w, lane, acc2, v2);
-      rk_mask(v2, m2);
-      rk_store(r.dh2 + (long)wr0 * H, H, live, h, g, c, v2);
-    });
-  }
-  rk_put(lds, w, lane, acc);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  rk_get(lds, w, lane, acc, v1);
-  rk_mask(v1, m1);
-  rk_store(r.dh1 + (long)wr0 * H, H, live, h, g, c, v1);
-  CLK_END(0);
-}
-
-// ppo_act_r: ActorCritic.act with the forward bits of the register row kernels (H = 256:
-// ppo_rows_k, or ppo_rows_r when HWY_ROWS_R == 1), for acting between updates whose minibatch
-// step runs them.  Every output element is the same chain of MFMAs
-// (weights as the A operand, k-blocks and k-steps in the same order, from zero), the same bias +
-// ReLU and the same head dot products and lane sums, so mean / value / log-prob are the bits the
-// step recomputes (ratio exactly 1 on the acted rows).  The work is split the other way round
-// for a rollout-sized batch: 16 rows per workgroup and the 16 output tiles of a layer over the 4
-// waves (4 each), the activations exchanged through a lane-linear LDS image (the B operand of
-// k-block kb for lane l at [kb][l]) between layers; each wave streams its own tiles' fragments
-// (global loads, 4 k-blocks ahead).  Wave 0 runs the head of all 16 rows.
-constexpr int kArD = 4;  // k-blocks of weight fragments in flight per wave
-__device__ __forceinline__ void ar_layer(const float* seg, int nblk, const f32x4* bimg, int lane,
-                                         int w, f32x4 (&acc)[4], f32x4 (&acc_o)[4]) {
-  const float* base = seg + (long)(4 * w) * nblk * 256 + 4 * lane;  // tile (4 w, 0), this lane
-  f32x4 ring[kArD][4];
-#pragma unroll
-  for (int d = 0; d < kArD; ++d)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      ring[d][i] = *reinterpret_cast<const f32x4*>(base + ((long)i * nblk + d) * 256);
-  for (int kb0 = 0; kb0 < nblk; kb0 += kArD) {  // nblk % kArD == 0 (rows_blocks)
-#pragma unroll
-    for (int d = 0; d < kArD; ++d) {
-      const int kb = kb0 + d;
-      const f32x4 b = bimg[kb * 64 + lane];
-      // ppo_rows_k: the even and the odd k-blocks in separate sums (kb0 % 4 == 0: parity of d)
-      f32x4 (&ac)[4] = (HWY_ROWS_R == 2 && (d & 1)) ? acc_o : acc;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          ac[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(ring[d][i][j], b[j], ac[i], 0, 0, 0);
-      const int kn = min(kb + kArD, nblk - 1);  // past the end: an in-range tile, never used
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        ring[d][i] = *reinterpret_cast<const f32x4*>(base + ((long)i * nblk + kn) * 256);
-    }
-  }
-}
-
-// bias + ReLU (rr_bias_relu's expression) of this wave's 4 output tiles into image `out`
-__device__ __forceinline__ void ar_epi(f32x4 (&acc)[4], f32x4 (&acc_o)[4], const float* bias,
-                                       f32x4* out, int w, int lane) {
-  const int g = lane >> 4;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int nb = 4 * w + i;
-    const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + 16 * nb + 4 * g);
-    if (HWY_ROWS_R == 2) acc[i] = acc[i] + acc_o[i];  // ppo_rows_k's even + odd partial sums
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float v = acc[i][q] + bv[q];
-      acc[i][q] = v > 0.0f ? v : 0.0f;
-    }
-    out[nb * 64 + lane] = acc[i];
-    acc[i] = acc_o[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  }
-}
-
-__global__ void __launch_bounds__(256) ppo_act_r(ActArgs r) {
-  constexpr int H = 256;
-  __shared__ __attribute__((aligned(16))) f32x4 img[3][16 * 64];  // three activation images
-  __shared__ __attribute__((aligned(16))) float tab[7 * 256];      // b1 b2 ba1 bc1 | wa2 0, 1, wc2
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, g = lane >> 4, c = lane & 15;
-  const int S = r.S;
-  const int row0 = blockIdx.x * 16;
-  const int nrows = min(16, r.B - row0);
-  const float* P = r.params;
-  int sb, hb;
-  rows_blocks(S, H, &sb, &hb);
-  const TileGeom T = tile_geom(S, H, sb, hb);
-  {
-    const int64_t bo[4] = {r.off[P_B1], r.off[P_B2], r.off[P_BA1], r.off[P_BC1]};
-#pragma unroll
-    for (int l = 0; l < 4; ++l) tab[l * 256 + t] = P[bo[l] + t];
-    tab[1024 + t] = P[r.off[P_WA2] + t];
-    tab[1280 + t] = P[r.off[P_WA2] + H + t];
-    tab[1536 + t] = P[r.off[P_WC2] + t];
-  }
-  // the states rows as layer 1's B operand image (k-block kb: lane (g, c) = x[row c][16 kb + 4 g ..])
-  for (int kb = w; kb < sb; kb += 4) {
-    const int k = 16 * kb + 4 * g;
-    f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (c < nrows && k < S) v = *reinterpret_cast<const f32x4*>(r.states + (long)(row0 + c) * S + k);
-    img[1][kb * 64 + lane] = v;
-  }
-  __syncthreads();
-  f32x4 acc[4], acc_o[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i] = acc_o[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  ar_layer(r.tiles + T.f1, sb, img[1], lane, w, acc, acc_o);
-  ar_epi(acc, acc_o, tab, img[0], w, lane);  // h1
-  __syncthreads();
-  ar_layer(r.tiles + T.f2, hb, img[0], lane, w, acc, acc_o);
-  ar_epi(acc, acc_o, tab + 256, img[1], w, lane);  // h2
-  __syncthreads();
-  ar_layer(r.tiles + T.fa, hb, img[1], lane, w, acc, acc_o);
-  ar_epi(acc, acc_o, tab + 512, img[0], w, lane);  // a1
-  ar_layer(r.tiles + T.fc, hb, img[1], lane, w, acc, acc_o);
-  ar_epi(acc, acc_o, tab + 768, img[2], w, lane);  // c1
-  __syncthreads();
-  if (w != 0) return;
-  // the head: the step's dot products (same order: ppo_rows_k sums each parity of the output
-  // tiles, lane-reduced, then the two), then act()'s sample of row c
-  float p0 = 0.0f, p1 = 0.0f, pv = 0.0f;
-  {
-    constexpr int NP = HWY_ROWS_R == 2 ? 2 : 1;  // parities summed separately
-    float pp[NP][3];
-#pragma unroll
-    for (int hp = 0; hp < NP; ++hp) {
-      float s0 = 0.0f, s1 = 0.0f, sv = 0.0f;
-#pragma unroll
-      for (int i = 0; i < 16 / NP; ++i) {
-        const int nb = NP * i + hp;
-        const f32x4 a1 = img[0][nb * 64 + lane], c1 = img[2][nb * 64 + lane];
-        const f32x4 x0 = *reinterpret_cast<const f32x4*>(tab + 1024 + 16 * nb + 4 * g);
-        const f32x4 x1 = *reinterpret_cast<const f32x4*>(tab + 1280 + 16 * nb + 4 * g);
-        const f32x4 xc = *reinterpret_cast<const f32x4*>(tab + 1536 + 16 * nb + 4 * g);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          s0 += a1[q] * x0[q];
-          s1 += a1[q] * x1[q];
-          sv += c1[q] * xc[q];
-        }
-      }
-      s0 += __shfl_xor(s0, 16), s1 += __shfl_xor(s1, 16), sv += __shfl_xor(sv, 16);
-      s0 += __shfl_xor(s0, 32), s1 += __shfl_xor(s1, 32), sv += __shfl_xor(sv, 32);
-      pp[hp][0] = s0, pp[hp][1] = s1, pp[hp][2] = sv;
-    }
-    p0 = pp[0][0], p1 = pp[0][1], pv = pp[0][2];
-    if (NP == 2) p0 = p0 + pp[NP - 1][0], p1 = p1 + pp[NP - 1][1], pv = pv + pp[NP - 1][2];
-  }
-  if (g != 0 || c >= nrows) return;
-  const long b = row0 + c;
-  const float ba0 = P[r.off[P_BA2]], ba1 = P[r.off[P_BA2] + 1], bcv = P[r.off[P_BC2]];
-  const float ls0 = P[r.off[P_LOGSTD]], ls1 = P[r.off[P_LOGSTD] + 1];
-  const float mu0 = p0 + ba0, mu1 = p1 + ba1, val = pv + bcv;
-  float z0 = mu0, z1 = mu1, lp = 0.0f;
-  if (r.noise) {
-    // torch Normal: scale = exp(log_std); var = scale**2; log_scale = log(scale)
-    const float sc0 = expf(ls0), sc1 = expf(ls1);
-    const float var0 = sc0 * sc0, var1 = sc1 * sc1;
-    const float lsc0 = logf(sc0), lsc1 = logf(sc1);
-    const float LOG_SQRT_2PI = 0.91893853320467274178f;
-    z0 = mu0 + sc0 * r.noise[2 * b];
-    z1 = mu1 + sc1 * r.noise[2 * b + 1];
-    const float d0 = z0 - mu0, d1 = z1 - mu1;
-    const float t0 = tanhf(z0), t1 = tanhf(z1);
-    const float lp0 = -(d0 * d0) / (2.0f * var0) - lsc0 - LOG_SQRT_2PI;
-    const float lp1 = -(d1 * d1) / (2.0f * var1) - lsc1 - LOG_SQRT_2PI;
-    lp = (lp0 - log1pf(-(t0 * t0) + 1e-6f)) + (lp1 - log1pf(-(t1 * t1) + 1e-6f));
-  }
-  r.action[2 * b] = tanhf(z0);
-  r.action[2 * b + 1] = tanhf(z1);
-  r.pre_tanh[2 * b] = z0;
-  r.pre_tanh[2 * b + 1] = z1;
-  r.logp[b] = lp;
-  r.value[b] = val;
-}
-
 // ----------------------------------------------------------------------------- weight grads
 // ppo_wgrad: every weight gradient of the minibatch step (the autograd of ppo/agent.py:241-248
 // for the four hidden layers), the bias column sums, the head-parameter sums over the ppo_rows
@@ -2789,6 +1814,8 @@ __device__ void wgrad_head(const WgArgs& a, int hid, float* lds, float* red) {
 }
 
 #define WG_ST(p, v) (*(p) = (v))  // (nontemporal partial stores measured slower in ppo_wsum)
+
+typedef __attribute__((address_space(3))) void lds_void_t;
 
 // ppo_wgrad's chunk loop with LDS-DMA staging (HWY_WG_DMA, the default).  Chunks of 64 rows go
 // global -> LDS by global_load_lds_dwordx4 (1 KB per wave instruction, no VGPRs, no VALU) into
@@ -3544,15 +2571,10 @@ __global__ void __launch_bounds__(kRedThreads) ppo_sumsq(const float* g, int64_t
 constexpr int kAdamEPT = HWY_ADAM_EPT;  // elements per thread (same box: 1 5.9 µs, 2 5.5, 4 5.7, 8 7.4)
 
 // clip_grad_norm_'s coefficient from the norm partials and Adam's bias corrections, into
-// sh[0] (coef), sh[1] (lr / bc1), sh[2] (sqrt bc2); every thread of the workgroup calls it.
-// SC1: the partials were stored by other workgroups of the same launch (ppo_wsum_adam), so they
-// are read with agent-scope loads (L1 bypassed) behind its grid barrier
-template <bool SC1 = false>
+// sh[0] (coef), sh[1] (lr / bc1), sh[2] (sqrt bc2); every thread of the workgroup calls it
 __device__ __forceinline__ void adam_scalars(const OptArgs& o, float* red, float* sh) {
   float s = 0.0f;
-  for (int k = threadIdx.x; k < o.nred; k += 256)
-    s += SC1 ? __hip_atomic_load(o.norm_part + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-             : o.norm_part[k];
+  for (int k = threadIdx.x; k < o.nred; k += 256) s += o.norm_part[k];
   s = wave_sum_dpp(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   if (threadIdx.x == 64) {  // wave 1, while the norm partials combine
@@ -3615,123 +2637,6 @@ __global__ void __launch_bounds__(256) ppo_adam(OptArgs o) {
   }
 }
 
-// ----------------------------------------------------------------------------- wsum + adam
-// ppo_wsum and ppo_adam in one launch, for a step with no gradient exchange between them
-// (hwy_ppo_step).  Workgroup i < nitems runs ppo_wsum's item i and keeps the gradient elements
-// it summed in registers; the workgroups after them take the head parameters' elements (summed
-// by ppo_wgrad's head workgroups).  Every thread loads its elements' Adam state and parameter
-// before the grid barrier, so that latency hides behind the barrier; clip_grad_norm_'s
-// coefficient then comes from the same norm partials in the same order as ppo_adam, so the
-// step's bits are those of ppo_wsum + ppo_adam.  The barrier needs every workgroup resident:
-// the host launches this kernel only when the grid fits the chip at its occupancy.
-struct WsaArgs {
-  WgArgs g;
-  OptArgs o;
-  uint32_t* bar;  // barrier words, each on its own 128-B line (wsa_grid_sync)
-  int nitems;     // ppo_wsum work items; gridDim.x - nitems head workgroups follow
-};
-constexpr int kWsaHeadPer = 4;  // head-parameter elements per thread
-#ifndef HWY_WSA_SLEEP
-#define HWY_WSA_SLEEP 2  // s_sleep between ppo_wsum_adam's barrier polls
-#endif
-
-// Grid barrier over the launch's (resident) workgroups, two levels: workgroup b arrives at
-// counter b % 8 (its own 128-B line), the last arrival there at the top counter, and the last of
-// those bumps the generation word the others poll (agent-scope loads, s_sleep between polls); each
-// counter returns to 0 with its last arrival.  Thread 0 arrives after every store of its workgroup
-// that another workgroup reads (the norm partial, an agent-scope store by thread 0 itself) has
-// completed.  The poll is bounded (~1 s), so a grid that is not resident ends instead of hanging
-// (its results are then wrong; the host prevents that case).
-constexpr int kWsaL1 = 8;  // first-level counters
-static_assert(32 * (kWsaL1 + 2) <= kBarF, "barrier words");
-__device__ __forceinline__ void wsa_grid_sync(uint32_t* bar) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t G = gridDim.x, k = blockIdx.x % kWsaL1;
-    const uint32_t nk = (G - k + kWsaL1 - 1) / kWsaL1;    // arrivals at counter k
-    const uint32_t ntop = G < kWsaL1 ? G : kWsaL1;          // counters in use
-    uint32_t* const top = bar + 32 * kWsaL1;
-    uint32_t* const gen = bar + 32 * (kWsaL1 + 1);
-    const uint32_t g0 = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the generation read and our stores
-    bool last = false;
-    if (__hip_atomic_fetch_add(bar + 32 * k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-        nk - 1) {
-      __hip_atomic_store(bar + 32 * k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ntop - 1) {
-        __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = true;
-      }
-    }
-    if (!last) {
-      for (int it = 0; it < (1 << 20); ++it) {
-        if (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != g0) break;
-        __builtin_amdgcn_s_sleep(HWY_WSA_SLEEP);
-      }
-    }
-  }
-  __syncthreads();
-}
-
-// flat index of head-parameter element e (0 .. 3H + 4): Wa2, ba2, log_std, Wc2, bc2
-__device__ __forceinline__ int64_t head_flat(const WgArgs& g, int e) {
-  const int H = g.H;
-  if (e < 2 * H) return g.off[P_WA2] + e;
-  if (e < 2 * H + 2) return g.off[P_BA2] + (e - 2 * H);
-  if (e < 2 * H + 4) return g.off[P_LOGSTD] + (e - 2 * H - 2);
-  if (e < 3 * H + 4) return g.off[P_WC2] + (e - 2 * H - 4);
-  return g.off[P_BC2];
-}
-
-__global__ void __launch_bounds__(256) ppo_wsum_adam(WsaArgs a) {
-  __shared__ float red[4];
-  __shared__ float sh[3];
-  const OptArgs& o = a.o;
-  constexpr int NE = 5;  // elements per thread: 4 tile elements + 1 bias, or kWsaHeadPer head
-  static_assert(kWsaHeadPer <= NE, "head elements per thread");
-  int64_t gi[NE];
-  float gv[NE], mo[NE], vo[NE], po[NE];
-#pragma unroll
-  for (int q = 0; q < NE; ++q) gi[q] = -1, gv[q] = 0.0f;
-  const bool item = (int)blockIdx.x < a.nitems;
-  if (item) {
-    WsumItem it;
-    wsum_item(a.g, blockIdx.x, it);
-    const float tot = block_sum4(it.sq, red);
-    if (threadIdx.x == 0)
-      __hip_atomic_store(a.g.norm_part + a.g.nh + blockIdx.x, tot, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-    for (int c4 = 0; c4 < 4; ++c4) gi[c4] = it.gi[c4], gv[c4] = it.v[c4];
-    gi[4] = it.bi, gv[4] = it.b;
-  } else {
-    const int nhe = 3 * a.g.H + 5;
-    const int e0 = ((int)blockIdx.x - a.nitems) * 256 * kWsaHeadPer;
-#pragma unroll
-    for (int q = 0; q < kWsaHeadPer; ++q) {
-      const int e = e0 + q * 256 + (int)threadIdx.x;
-      if (e < nhe) {
-        gi[q] = head_flat(a.g, e);
-        gv[q] = o.grads[gi[q]];  // written by ppo_wgrad (the previous launch)
-      }
-    }
-  }
-  // the elements' Adam state and parameters, in flight across the barrier
-#pragma unroll
-  for (int q = 0; q < NE; ++q) {
-    const int64_t i = gi[q] >= 0 ? gi[q] : 0;
-    mo[q] = o.m[i], vo[q] = o.v[i], po[q] = o.params[i];
-  }
-  wsa_grid_sync(a.bar);
-  adam_scalars<true>(o, red, sh);
-#pragma unroll
-  for (int q = 0; q < NE; ++q)
-    if (gi[q] >= 0) adam_elem(o, gi[q], gv[q], mo[q], vo[q], po[q], sh);
-}
-
 template <int AM, int BM, int EPI>
 int launch_gemm(const GemmArgs& g, int splits, hipStream_t s) {
   dim3 grid((g.M + kTile - 1) / kTile, (g.N + kTile - 1) / kTile, splits);
@@ -3780,88 +2685,6 @@ int64_t hwy_ppo_tile_image_offset(const hwy_ppo_dims* d) {
   return (int64_t)(reinterpret_cast<char*>(w.wtile) - base);
 }
 
-// ppo_rows + ppo_wgrad of the fused path (the ppo_wgrad arguments returned for ppo_wsum)
-static int fused_rows_wgrad(const hwy_ppo_args* a, const Work& w, const Layout& L, hipStream_t s,
-                            WgArgs& g) {
-  const hwy_ppo_dims& d = a->dims;
-  const int B = d.B, S = d.S, H = d.H;
-  const float* P = a->params;
-  int rc = 0;
-  RowArgs r = {};
-  r.B = B, r.S = S;
-  r.states = a->states, r.idx = a->idx, r.pre_tanh = a->pre_tanh, r.old_logp = a->old_logp;
-  r.adv = a->adv, r.ret = a->ret, r.params = P;
-  for (int i = 0; i < 13; ++i) r.off[i] = L.off[i];
-  r.h1 = w.h1, r.h2 = w.h2, r.dac = w.dac, r.dh2 = w.dh2, r.dh1 = w.dh1, r.xg = w.xg;
-  r.tiles = w.wtile;
-  r.head_part = w.head_part, r.HP = w.HP;
-  r.eps_clip = a->eps_clip, r.value_coef = a->value_coef, r.entropy_coef = a->entropy_coef;
-  r.counters = a->counters;
-  // 8 waves (2 per SIMD) when the columns split into 16-wide tiles, else 4
-  const dim3 g1(w.n1), b4(256), b8(512);
-  if (w.rt == 4 * kRowTile && HWY_ROWS_R == 2) {
-    const dim3 bk(64 * kRkWaves);
-    switch (w.sb) {
-      case 4: hipLaunchKernelGGL((ppo_rows_k<4>), g1, bk, 0, s, r); break;
-      case 8: hipLaunchKernelGGL((ppo_rows_k<8>), g1, bk, 0, s, r); break;
-      case 12: hipLaunchKernelGGL((ppo_rows_k<12>), g1, bk, 0, s, r); break;
-      default: hipLaunchKernelGGL((ppo_rows_k<16>), g1, bk, 0, s, r); break;
-    }
-  } else if (w.rt == 4 * kRowTile && HWY_ROWS_R == 1) {
-    const dim3 br(64 * kRrWaves);
-    switch (w.sb) {
-      case 4: hipLaunchKernelGGL((ppo_rows_r<4>), g1, br, 0, s, r); break;
-      case 8: hipLaunchKernelGGL((ppo_rows_r<8>), g1, br, 0, s, r); break;
-      case 12: hipLaunchKernelGGL((ppo_rows_r<12>), g1, br, 0, s, r); break;
-      default: hipLaunchKernelGGL((ppo_rows_r<16>), g1, br, 0, s, r); break;
-    }
-  } else if (w.rt == 4 * kRowTile) {
-    hipLaunchKernelGGL((ppo_rows_c64<4, 8>), g1, b8, 0, s, r);
-  } else if (w.rt == 2 * kRowTile) {
-    switch (H / 64) {
-      case 1: hipLaunchKernelGGL((ppo_rows<1, 4, 32>), g1, b4, 0, s, r); break;
-      case 2: hipLaunchKernelGGL((ppo_rows<2, 8, 32>), g1, b8, 0, s, r); break;
-      case 3: hipLaunchKernelGGL((ppo_rows<3, 4, 32>), g1, b4, 0, s, r); break;
-      default:
-        if (HWY_ROWS_CMP && HWY_ROWS_NW32 == 8)
-          hipLaunchKernelGGL((ppo_rows_c<4, 8, 32>), g1, b8, 0, s, r);
-        else
-          hipLaunchKernelGGL((ppo_rows<4, HWY_ROWS_NW32, 32>), g1, dim3(64 * HWY_ROWS_NW32), 0, s, r);
-        break;
-    }
-  } else {
-    switch (H / 64) {
-      case 1: hipLaunchKernelGGL((ppo_rows<1, 4, 16>), g1, b4, 0, s, r); break;
-      case 2: hipLaunchKernelGGL((ppo_rows<2, 8, 16>), g1, b8, 0, s, r); break;
-      case 3: hipLaunchKernelGGL((ppo_rows<3, 4, 16>), g1, b4, 0, s, r); break;
-      case 4: hipLaunchKernelGGL((ppo_rows<4, HWY_ROWS_NW, 16>), g1, dim3(64 * HWY_ROWS_NW), 0, s, r); break;
-      case 5: hipLaunchKernelGGL((ppo_rows<5, 4, 16>), g1, b4, 0, s, r); break;
-      case 6: hipLaunchKernelGGL((ppo_rows<6, 8, 16>), g1, b8, 0, s, r); break;
-      case 7: hipLaunchKernelGGL((ppo_rows<7, 4, 16>), g1, b4, 0, s, r); break;
-      default: hipLaunchKernelGGL((ppo_rows<8, 8, 16>), g1, b8, 0, s, r); break;
-    }
-  }
-  rc |= hipGetLastError() == hipSuccess ? 0 : -1;
-  g = WgArgs{};
-  g.B = B, g.S = S, g.H = H;
-  g.dac = w.dac, g.h2 = w.h2, g.dh2 = w.dh2, g.h1 = w.h1, g.dh1 = w.dh1, g.xg = w.xg;
-  g.grads = a->grads;
-  for (int i = 0; i < 13; ++i) g.off[i] = L.off[i];
-  g.head_part = w.head_part, g.nhp = w.n1, g.HP = w.HP, g.norm_part = w.norm_part;
-  g.tac = w.tac, g.t2 = w.t2, g.t1 = w.t1, g.nh = w.nh;
-  g.split = w.split, g.slab = w.wg_slab;
-  g.bal = w.bal, g.wm = w.wm, g.tpe = w.tpe, g.nslot = w.nslot;
-  g.entropy_coef = a->entropy_coef, g.value_coef = a->value_coef;
-  g.ent_const = 0.5f + 0.91893853320467274178f;
-  g.params = P, g.metrics = a->metrics, g.counters = a->counters;
-  hipLaunchKernelGGL(ppo_wgrad, dim3(w.grid2), dim3(64 * kWgWaves), 0, s, g);
-  rc |= hipGetLastError() == hipSuccess ? 0 : -1;
-  return rc;
-}
-
-// ppo_wsum's work items (1024 elements of a weight-gradient tile each)
-static int wsum_items(const Work& w) { return (w.tac + w.t2 + w.t1) * (kWgTM * kWgTN / 1024); }
-
 int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
   if (!a) return -1;
   const hwy_ppo_dims& d = a->dims;
@@ -3873,9 +2696,60 @@ int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
   const float* P = a->params;
   int rc = 0;
   if (w.fused) {
-    WgArgs g;
-    rc |= fused_rows_wgrad(a, w, L, s, g);
-    hipLaunchKernelGGL(ppo_wsum, dim3(wsum_items(w)), dim3(256), 0, s, g);
+    RowArgs r = {};
+    r.B = B, r.S = S;
+    r.states = a->states, r.idx = a->idx, r.pre_tanh = a->pre_tanh, r.old_logp = a->old_logp;
+    r.adv = a->adv, r.ret = a->ret, r.params = P;
+    for (int i = 0; i < 13; ++i) r.off[i] = L.off[i];
+    r.h1 = w.h1, r.h2 = w.h2, r.dac = w.dac, r.dh2 = w.dh2, r.dh1 = w.dh1, r.xg = w.xg;
+    r.tiles = w.wtile;
+    r.head_part = w.head_part, r.HP = w.HP;
+    r.eps_clip = a->eps_clip, r.value_coef = a->value_coef, r.entropy_coef = a->entropy_coef;
+    r.counters = a->counters;
+    // 8 waves (2 per SIMD) when the columns split into 16-wide tiles, else 4
+    const dim3 g1(w.n1), b4(256), b8(512), blk(256);
+    if (w.rt == 4 * kRowTile) {
+      hipLaunchKernelGGL((ppo_rows_c64<4, 8>), g1, b8, 0, s, r);
+    } else if (w.rt == 2 * kRowTile) {
+      switch (H / 64) {
+        case 1: hipLaunchKernelGGL((ppo_rows<1, 4, 32>), g1, b4, 0, s, r); break;
+        case 2: hipLaunchKernelGGL((ppo_rows<2, 8, 32>), g1, b8, 0, s, r); break;
+        case 3: hipLaunchKernelGGL((ppo_rows<3, 4, 32>), g1, b4, 0, s, r); break;
+        default:
+          if (HWY_ROWS_CMP && HWY_ROWS_NW32 == 8)
+            hipLaunchKernelGGL((ppo_rows_c<4, 8, 32>), g1, b8, 0, s, r);
+          else
+            hipLaunchKernelGGL((ppo_rows<4, HWY_ROWS_NW32, 32>), g1, dim3(64 * HWY_ROWS_NW32), 0, s, r);
+          break;
+      }
+    } else {
+      switch (H / 64) {
+        case 1: hipLaunchKernelGGL((ppo_rows<1, 4, 16>), g1, b4, 0, s, r); break;
+        case 2: hipLaunchKernelGGL((ppo_rows<2, 8, 16>), g1, b8, 0, s, r); break;
+        case 3: hipLaunchKernelGGL((ppo_rows<3, 4, 16>), g1, b4, 0, s, r); break;
+        case 4: hipLaunchKernelGGL((ppo_rows<4, HWY_ROWS_NW, 16>), g1, dim3(64 * HWY_ROWS_NW), 0, s, r); break;
+        case 5: hipLaunchKernelGGL((ppo_rows<5, 4, 16>), g1, b4, 0, s, r); break;
+        case 6: hipLaunchKernelGGL((ppo_rows<6, 8, 16>), g1, b8, 0, s, r); break;
+        case 7: hipLaunchKernelGGL((ppo_rows<7, 4, 16>), g1, b4, 0, s, r); break;
+        default: hipLaunchKernelGGL((ppo_rows<8, 8, 16>), g1, b8, 0, s, r); break;
+      }
+    }
+    rc |= hipGetLastError() == hipSuccess ? 0 : -1;
+    WgArgs g = {};
+    g.B = B, g.S = S, g.H = H;
+    g.dac = w.dac, g.h2 = w.h2, g.dh2 = w.dh2, g.h1 = w.h1, g.dh1 = w.dh1, g.xg = w.xg;
+    g.grads = a->grads;
+    for (int i = 0; i < 13; ++i) g.off[i] = L.off[i];
+    g.head_part = w.head_part, g.nhp = w.n1, g.HP = w.HP, g.norm_part = w.norm_part;
+    g.tac = w.tac, g.t2 = w.t2, g.t1 = w.t1, g.nh = w.nh;
+    g.split = w.split, g.slab = w.wg_slab;
+    g.bal = w.bal, g.wm = w.wm, g.tpe = w.tpe, g.nslot = w.nslot;
+    g.entropy_coef = a->entropy_coef, g.value_coef = a->value_coef;
+    g.ent_const = 0.5f + 0.91893853320467274178f;
+    g.params = P, g.metrics = a->metrics, g.counters = a->counters;
+    hipLaunchKernelGGL(ppo_wgrad, dim3(w.grid2), dim3(64 * kWgWaves), 0, s, g);
+    rc |= hipGetLastError() == hipSuccess ? 0 : -1;
+    hipLaunchKernelGGL(ppo_wsum, dim3((w.tac + w.t2 + w.t1) * (kWgTM * kWgTN / 1024)), blk, 0, s, g);
     rc |= hipGetLastError() == hipSuccess ? 0 : -1;
     return rc;
   }
@@ -3994,23 +2868,6 @@ int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
   return rc;
 }
 
-static OptArgs opt_args(const hwy_ppo_args* a, const Work& w, const Layout& L) {
-  const hwy_ppo_dims& d = a->dims;
-  OptArgs o = {};
-  o.params = a->params, o.grads = a->grads, o.m = a->adam_m, o.v = a->adam_v;
-  // norm partials: ppo_sumsq / ppo_reduce write nred of them, ppo_wgrad + ppo_wsum nred2
-  o.norm_part = w.norm_part, o.numel = L.numel, o.counters = a->counters;
-  o.nred = (w.fused && !a->grads_modified) ? w.nred2 : w.nred;
-  o.lr = a->lr, o.beta1 = a->beta1, o.beta2 = a->beta2, o.eps = a->adam_eps;
-  o.max_norm = a->max_grad_norm;
-  if (w.fused) {
-    o.tiles = w.wtile;
-    o.o_w1 = L.off[P_W1], o.o_w2 = L.off[P_W2], o.o_wa1 = L.off[P_WA1], o.o_wc1 = L.off[P_WC1];
-    o.S = d.S, o.H = d.H, o.sb = w.sb, o.hb = w.hb;
-  }
-  return o;
-}
-
 int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream) {
   if (!a) return -1;
   const hwy_ppo_dims& d = a->dims;
@@ -4023,49 +2880,21 @@ int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream) {
                        w.norm_part);
     if (hipGetLastError() != hipSuccess) return -1;
   }
-  const OptArgs o = opt_args(a, w, L);
+  OptArgs o = {};
+  o.params = a->params, o.grads = a->grads, o.m = a->adam_m, o.v = a->adam_v;
+  // norm partials: ppo_sumsq / ppo_reduce write nred of them, ppo_wgrad grid2
+  o.norm_part = w.norm_part, o.numel = L.numel, o.counters = a->counters;
+  o.nred = (w.fused && !a->grads_modified) ? w.nred2 : w.nred;
+  o.lr = a->lr, o.beta1 = a->beta1, o.beta2 = a->beta2, o.eps = a->adam_eps;
+  o.max_norm = a->max_grad_norm;
+  if (w.fused) {
+    o.tiles = w.wtile;
+    o.o_w1 = L.off[P_W1], o.o_w2 = L.off[P_W2], o.o_wa1 = L.off[P_WA1], o.o_wc1 = L.off[P_WC1];
+    o.S = d.S, o.H = d.H, o.sb = w.sb, o.hb = w.hb;
+  }
   const int nadam = (int)((L.numel + 256 * kAdamEPT - 1) / (256 * kAdamEPT));
   hipLaunchKernelGGL(ppo_adam, dim3(nadam), dim3(256), 0, s, o);
   return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-// ppo_wsum_adam's grid (ppo_wsum's items + the head-parameter workgroups), or 0 when it would
-// not be resident on the chip at the kernel's occupancy (its grid barrier needs every workgroup
-// running at once): the step then launches ppo_wsum and ppo_adam
-static int wsa_grid(const Work& w, int H) {
-  static int occ = -1;
-  if (occ < 0) {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ppo_wsum_adam, 256, 0) != hipSuccess) {
-      (void)hipGetLastError();
-      n = 0;
-    }
-    occ = n;
-  }
-  const int grid = wsum_items(w) + (3 * H + 5 + 256 * kWsaHeadPer - 1) / (256 * kWsaHeadPer);
-  return grid <= occ * chip_geom().cus ? grid : 0;
-}
-
-int hwy_ppo_step(const hwy_ppo_args* a, void* stream) {
-  if (!a) return -1;
-  const hwy_ppo_dims& d = a->dims;
-  if (hwy_ppo_workspace_bytes(&d) < 0) return -1;
-  const Work w = carve(d, a->workspace, nullptr);
-  const int grid = w.fused && !a->grads_modified && !dev_knob_int("HWY_WSA_OFF", 0) ? wsa_grid(w, d.H) : 0;
-  if (!grid) {
-    const int rc = hwy_ppo_forward_backward(a, stream);
-    return rc | hwy_ppo_optimizer(a, stream);
-  }
-  hipStream_t s = (hipStream_t)stream;
-  const Layout L = make_layout(d);
-  WsaArgs x = {};
-  int rc = fused_rows_wgrad(a, w, L, s, x.g);
-  x.o = opt_args(a, w, L);
-  x.bar = w.bar;
-  x.nitems = wsum_items(w);
-  hipLaunchKernelGGL(ppo_wsum_adam, dim3(grid), dim3(256), 0, s, x);
-  rc |= hipGetLastError() == hipSuccess ? 0 : -1;
-  return rc;
 }
 
 int hwy_ppo_sync_params(const hwy_ppo_args* a, void* stream) {
@@ -4083,9 +2912,7 @@ int hwy_ppo_sync_params(const hwy_ppo_args* a, void* stream) {
   const int64_t n = tile_geom(d.S, d.H, w.sb, w.hb).total;
   hipLaunchKernelGGL(ppo_retile, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, t);
-  if (hipGetLastError() != hipSuccess) return -1;
-  // ppo_wsum_adam's barrier words start from 0 (its arrivals counter returns to 0 every launch)
-  return hipMemsetAsync(w.bar, 0, kBarF * sizeof(float), (hipStream_t)stream) == hipSuccess ? 0 : -1;
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int hwy_ppo_act(const hwy_ppo_act_args* a, void* stream) {
@@ -4116,11 +2943,7 @@ int hwy_ppo_act(const hwy_ppo_act_args* a, void* stream) {
   };
   // H = 256 from the tile image: the compact kernel, 32-row tiles once there are two per CU
   // (16,384 rows on MI355X: 91.3 -> 69.4 us), else 16-row tiles (4,096 rows: 25.1 -> 22.0 us)
-  if (HWY_ROWS_R > 0 && r.tiles && d.H == 256 && a->learner_rows > 0 &&
-      rows_tile(a->learner_rows, d.H) == 4 * kRowTile) {
-    // the learner's minibatch step runs ppo_rows_r: act with its forward bits
-    hipLaunchKernelGGL(ppo_act_r, dim3((d.B + 15) / 16), dim3(256), 0, s, r);
-  } else if (HWY_ACT_CMP && r.tiles && d.H == 256) {
+  if (HWY_ACT_CMP && r.tiles && d.H == 256) {
     if (d.B >= 64 * chip_geom().cus)
       hipLaunchKernelGGL((ppo_act_c<4, 8, 32>), dim3((d.B + 31) / 32), b8, 0, s, r);
     else

@@ -51,7 +51,7 @@ class PpoActArgs(ctypes.Structure):
         ("dims", PpoDims),
         ("states", ctypes.c_void_p), ("params", ctypes.c_void_p), ("noise", ctypes.c_void_p),
         ("action", ctypes.c_void_p), ("pre_tanh", ctypes.c_void_p), ("logp", ctypes.c_void_p),
-        ("value", ctypes.c_void_p), ("tiles", ctypes.c_void_p), ("learner_rows", ctypes.c_int32),
+        ("value", ctypes.c_void_p), ("tiles", ctypes.c_void_p),
     ]
 
 
@@ -66,8 +66,6 @@ def _bind(L):
     L.hwy_ppo_forward_backward.restype = ctypes.c_int
     L.hwy_ppo_optimizer.argtypes = [ctypes.POINTER(PpoArgs), ctypes.c_void_p]
     L.hwy_ppo_optimizer.restype = ctypes.c_int
-    L.hwy_ppo_step.argtypes = [ctypes.POINTER(PpoArgs), ctypes.c_void_p]
-    L.hwy_ppo_step.restype = ctypes.c_int
     L.hwy_ppo_sync_params.argtypes = [ctypes.POINTER(PpoArgs), ctypes.c_void_p]
     L.hwy_ppo_sync_params.restype = ctypes.c_int
     L.hwy_ppo_act.argtypes = [ctypes.POINTER(PpoActArgs), ctypes.c_void_p]
@@ -218,8 +216,6 @@ def fused_act(agent, states: torch.Tensor, deterministic: bool = False,
     a.tiles = F.current_tiles(flat) if F is not None else None
     if a.tiles is None and H == _ACT_C_HIDDEN:
         a.tiles = _act_tiles(agent, flat, S, H)
-    # acting reproduces the forward bits of the minibatch step of the agent's fused learner
-    a.learner_rows = F.mb if F is not None and F.flat is flat else 0
     check(_bind(lib()).hwy_ppo_act(ctypes.byref(a), stream_ptr()), "hwy_ppo_act")
     return action, pre, logp, value
 
@@ -259,10 +255,6 @@ class FusedPPO:
         self.capture_collectives = self._rccl and os.environ.get("HWY_GRAPH_COLLECTIVES", "1") != "0"
         self._captured_collectives = False
         self.use_graphs = use_graphs
-        # True: one-process steps go through hwy_ppo_step (the gradient-tile sums and Adam as one
-        # launch behind a grid barrier; the same bits); measured 1.5-2.5 us per step slower than
-        # hwy_ppo_forward_backward + hwy_ppo_optimizer, so off
-        self.single_call = False
         self._import_torch_state()
         self._graphs = None
         self._bound_key = None
@@ -342,14 +334,6 @@ class FusedPPO:
     def _opt(self, a):
         check(self.L.hwy_ppo_optimizer(ctypes.byref(a), stream_ptr()), "hwy_ppo_optimizer")
 
-    def _step(self, a):
-        """One minibatch step with no gradient exchange: forward/backward and the optimizer."""
-        if self.single_call:
-            check(self.L.hwy_ppo_step(ctypes.byref(a), stream_ptr()), "hwy_ppo_step")
-        else:
-            self._fwd_bwd(a)
-            self._opt(a)
-
     def sync_params(self, a):
         """Rebuild the workspace's weight tile image from the flat params (hwy_ppo_sync_params);
         needed before a step whenever params changed outside hwy_ppo_optimizer."""
@@ -415,15 +399,12 @@ class FusedPPO:
         if not self.use_graphs:
             for _ in range(epochs):
                 for a in args:
-                    if self.group is None:
-                        self._step(a)
-                        continue
                     self._fwd_bwd(a)
-                    self._allreduce()
+                    if self.group is not None:
+                        self._allreduce()
                     self._opt(a)
             self._tiles_version = self._param_versions()
             return self.metrics
-        key = key + (self.single_call,)
         if self._graphs is None or self._bound_key != key:
             self._capture(args)
             self._bound_key = key
@@ -461,7 +442,8 @@ class FusedPPO:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=s):
                     for a in args:
-                        self._step(a)
+                        self._fwd_bwd(a)
+                        self._opt(a)
                 graphs.append(g)
             else:
                 for a in args:

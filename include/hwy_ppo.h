@@ -72,14 +72,7 @@ typedef struct hwy_ppo_args {
 int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream);
 /* clip_grad_norm_(max_grad_norm) + Adam step on params (call after any gradient all-reduce). */
 int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream);
-/* One whole minibatch step: hwy_ppo_forward_backward then hwy_ppo_optimizer, for a step with no
- * gradient exchange between them (grads_modified == 0).  On the fused path the gradient-tile
- * sums and the Adam step run as one launch (a grid barrier between them); grads, params, Adam
- * state, the tile image and the metrics row end bit-identical to the two calls.  Replaces the
- * same reference body as the pair (ppo/agent.py:216-252). */
-int hwy_ppo_step(const hwy_ppo_args* a, void* stream);
-/* Rebuild the workspace's weight tile image from params (uses dims, params, workspace); also
- * resets the workspace's step-synchronisation words (call it once before the first step). */
+/* Rebuild the workspace's weight tile image from params (uses dims, params, workspace). */
 int hwy_ppo_sync_params(const hwy_ppo_args* a, void* stream);
 
 /* Byte offset of the weight tile image inside a workspace for dims (-1 when the dims take
@@ -104,8 +97,6 @@ typedef struct hwy_ppo_act_args {
   float* logp;     /* [B] */
   float* value;    /* [B] */
   const float* tiles; /* optional weight tile image (see above), or NULL */
-  int32_t learner_rows; /* minibatch rows of the hwy_ppo step whose forward bits acting should
-                           reproduce (its ratio is then exactly 1 on the acted rows), 0 unknown */
 } hwy_ppo_act_args;
 int hwy_ppo_act(const hwy_ppo_act_args* a, void* stream);
 

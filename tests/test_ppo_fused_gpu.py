@@ -191,8 +191,8 @@ def _check_grads(ga, gb, g64, msg=""):
                                     # 32-row ppo_rows workgroups (4 or 8 waves) at the narrower
                                     # learners, H 64 / 128 / 192, with the balanced wgrad split
                                     (60, 64, 16384), (60, 128, 16384), (136, 192, 16384),
-                                    # ppo_rows_r (64-row tiles, H 256) with a ragged last
-                                    # workgroup (16 rows), its 12-block states width (S 180)
+                                    # 64-row ppo_rows_c64 tiles with a ragged last workgroup
+                                    # (16 rows), and its 12-block states width (S 180)
                                     (60, 256, 16400), (180, 256, 16400)])
 def test_fused_gradient_matches_autograd(S, H, mb):
     """One fused forward/backward against autograd on the same minibatch.  The reference
@@ -250,34 +250,6 @@ def test_fused_update_matches_torch_update(graphs):
         assert (d > 2e-5).float().mean().item() < 0.05, (k, d.max().item())
     torch.testing.assert_close(rows_b, rows_a, rtol=5e-3, atol=5e-5)
     assert int(F.counters[0]) == steps
-
-
-@pytest.mark.parametrize("S,H,n,nmb,graphs", [(60, 256, 32768, 2, True),   # 64-row tiles
-                                               (60, 256, 2048, 4, False),   # 16-row tiles
-                                               (120, 384, 32768, 2, True),
-                                               (240, 512, 8192, 1, False)])
-def test_single_call_step_equals_two_calls(S, H, n, nmb, graphs):
-    """hwy_ppo_step (ppo_wsum + ppo_adam as one launch behind a grid barrier) against
-    hwy_ppo_forward_backward + hwy_ppo_optimizer on the same update: every output bit-equal --
-    params, grads, Adam moments, step counter, metrics rows and the weight tile image."""
-    _, b1 = _agents(S, H, epochs=2)
-    _, b2 = _agents(S, H, epochs=2)
-    s, z, lp, adv, ret, perm = _data(n, S, b1)
-    mb = n // nmb
-    out = []
-    for b, single in ((b1, False), (b2, True)):
-        F = FusedPPO(b, mb, nmb, use_graphs=graphs)
-        F.single_call = single
-        rows = F.run(s, z, lp, adv.clone(), ret.clone(), perm.clone()).clone()
-        torch.cuda.synchronize()
-        # the tile image runs to the workspace's last 1,280 B (the step's barrier words)
-        tiles = F.workspace[F._tile_off:-1280].clone() if F._tile_off is not None else None
-        out.append((F.flat.clone(), F.grads.clone(), F.m.clone(), F.v.clone(), rows,
-                    F.counters.clone(), tiles))
-    for x, y, name in zip(out[0], out[1], ("params", "grads", "m", "v", "metrics", "counters", "tiles")):
-        if x is None:
-            continue
-        assert torch.equal(x, y), name
 
 
 @pytest.mark.parametrize("S,H,n,nmb,epochs", [(60, 256, 2048, 4, 3),
@@ -559,14 +531,12 @@ def test_fused_act_from_tile_image_equals_params_path(S, H):
         torch.testing.assert_close(g, r, rtol=1e-4, atol=2e-5)
 
 
-@pytest.mark.parametrize("S,B", [(60, 16384), (120, 20000), (60, 16390), (240, 16384), (60, 4096),
-                                 (120, 1000)])
+@pytest.mark.parametrize("S,B", [(60, 16384), (120, 20000), (60, 4096), (120, 1000)])
 def test_compact_act_kernel(S, B):
-    """The H = 256 acting kernels from the tile image -- ppo_act_r when the agent's learner runs
-    ppo_rows_r (minibatches of >= 64 rows per CU: the first four cases, one with a ragged last
-    workgroup), else ppo_act_c -- against ActorCritic.act with the same draws and against the
-    params path; and the acting forward is the minibatch step's, so re-evaluating the acted rows
-    in a fused step gives a ratio of exactly 1 on every row (KL and clip count exactly 0)."""
+    """ppo_act_c (H 256, tile image in step; 32-row tiles from two per CU, else 16): against
+    ActorCritic.act with the same draws and against ppo_act on the params path; and its head is
+    the minibatch step's, so re-evaluating the acted rows in a fused step gives a ratio of
+    exactly 1 on every row (KL and clip count exactly 0)."""
     from hwy.ppo_native import fused_act
 
     H, n = 256, min(B, 16384)

@@ -27,7 +27,6 @@ adv = torch.randn(n, device=dev)
 ret = torch.randn(n, device=dev)
 perm = torch.randperm(n, device=dev)
 F = FusedPPO(ag, mb, nmb, use_graphs=True)
-F.single_call = os.environ.get("HWY_SPLIT_STEP", "0") != "1"  # 1: forward_backward + optimizer
 F.run(s, z, lp, adv, ret, perm)
 torch.cuda.synchronize()
 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
