@@ -181,13 +181,6 @@ __device__ unsigned long long g_hwy_wave_t[5 * HWY_NWT];
 #ifndef HWY_SKIP
 #define HWY_SKIP 0
 #endif
-// Branch-free frame bodies: the IDM, steering and vehicle-step arithmetic that some lane of every
-// env executes anyway (the actors, the present vehicles) runs on every lane and the results are
-// selected, instead of under an exec-mask branch (s_and_saveexec / s_cbranch_execz / restore per
-// if); the selected lanes compute exactly the same operations, so the state bits do not change
-#ifndef HWY_BRANCHFREE
-#define HWY_BRANCHFREE 1
-#endif
 
 // ------------------------------------------------------------------------- vehicle state
 struct Veh {
@@ -241,12 +234,6 @@ __device__ __forceinline__ float idm_free(float ev_spd, float ev_tsp, float delt
 __device__ __forceinline__ float idm_with_front(float acc, float ev_spd, float ev_x, float ev_c,
                                                 float ev_s, bool has_front, float fv_x,
                                                 float fv_spd, float fv_c, float fv_s) {
-  if (HWY_BRANCHFREE) {  // the interaction term on every lane, kept where there is a front
-    const float d = fv_x - ev_x;
-    const float g = desired_gap(ev_spd, ev_c, ev_s, fv_spd, fv_c, fv_s) / hm_not_zero(d);
-    const float af = hm_fma(-COMFORT_ACC_MAX, g * g, acc);
-    return has_front ? af : acc;
-  }
   if (has_front) {
     float d = fv_x - ev_x;
     float g = desired_gap(ev_spd, ev_c, ev_s, fv_spd, fv_c, fv_s) / hm_not_zero(d);
@@ -878,10 +865,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   float self_a = 0.0f;
   // (the free-road term is shared by every acceleration(self, .) evaluated this frame)
   float a_free = 0.0f;
-  if (HWY_BRANCHFREE) {  // every lane (only the actors' values are used)
-    a_free = idm_free(v.spd, v.tsp, v.dlt, limit);
-    self_a = idm_with_front(a_free, v.spd, v.x, ch, sh, fi[1] >= 0, op_x, op_spd, op_c, op_s);
-  } else if (actor) {
+  if (actor) {
     a_free = idm_free(v.spd, v.tsp, v.dlt, limit);
     self_a = idm_with_front(a_free, v.spd, v.x, ch, sh, fi[1] >= 0, op_x, op_spd, op_c, op_s);
   }
@@ -977,15 +961,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   const int st_ = ft >= 0 ? ft : lane;
   const float ft_x = shf(v.x, st_), ft_spd = shf(v.spd, st_), ft_c = shf(ch, st_),
               ft_s = shf(sh, st_);
-  if (HWY_BRANCHFREE) {  // every lane, kept on the actors
-    const float steer = (HWY_SKIP & 16) ? 0.0f : steering_tan(v.y, v.h, v.spd, v.tl);
-    const float acc_t =
-        idm_with_front(a_free, v.spd, v.x, ch, sh, ft >= 0, ft_x, ft_spd, ft_c, ft_s);
-    float acc = need_t ? hm_minf(self_a, acc_t) : self_a;
-    acc = hm_clipf(acc, -ACC_MAX, ACC_MAX);
-    v.asteer = actor ? steer : v.asteer;
-    v.aacc = actor ? acc : v.aacc;
-  } else if (actor) {
+  if (actor) {
     const float steer = (HWY_SKIP & 16) ? 0.0f : steering_tan(v.y, v.h, v.spd, v.tl);
     float acc = self_a;
     if (need_t) {
@@ -1000,35 +976,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
 
   SEC(sp, 5);
   // ---------------- Road.step: Vehicle.step for every vehicle
-  if (HWY_BRANCHFREE) {  // every lane; the present vehicles take the results
-    const bool pr = v.present;
-    const float tmr = lane != 0 ? v.tmr + dt : v.tmr;  // IDMVehicle.step
-    const float asteer = v.crashed ? 0.0f : v.asteer;  // clip_actions
-    float aacc = v.crashed ? -1.0f * v.spd : v.aacc;
-    aacc = v.spd > MAX_SPEED   ? hm_minf(aacc, 1.0f * (MAX_SPEED - v.spd))
-           : v.spd < MIN_SPEED ? hm_maxf(aacc, 1.0f * (MIN_SPEED - v.spd))
-                               : aacc;
-    const float u = 0.5f * ((lane == 0 && !v.crashed) ? tan_ego : asteer);
-    const float cb = 1.0f / __builtin_sqrtf(hm_fma(u, u, 1.0f));
-    const float sb = u * cb;
-    const float cdir = hm_fma(ch, cb, -(sh * sb));
-    const float sdir = hm_fma(sh, cb, ch * sb);
-    const float vx = v.spd * cdir;
-    const float vy = v.spd * sdir;
-    float x = hm_fma(vx, dt, v.x);
-    float y = hm_fma(vy, dt, v.y);
-    x = v.imp ? x + v.ix : x;
-    y = v.imp ? y + v.iy : y;
-    const float hn = hm_fma(v.spd * sb, dt * (2.0f / VEH_LENGTH), v.h);  // speed sin(beta) / (L/2) dt
-    const float spd = hm_fma(aacc, dt, v.spd);
-    const int ln = closest_lane(y, lanes);  // on_state_update
-    if (pr) {
-      v.tmr = tmr, v.asteer = asteer, v.aacc = aacc, v.x = x, v.y = y, v.h = hn, v.spd = spd;
-      v.ln = ln;
-      v.crashed = v.crashed || v.imp;
-      v.imp = false;
-    }
-  } else if (v.present) {
+  if (v.present) {
     if (lane != 0) v.tmr = v.tmr + dt;  // IDMVehicle.step
     if (v.crashed) {                    // clip_actions
       v.asteer = 0.0f;
