@@ -1275,7 +1275,7 @@ __global__ void __launch_bounds__(256) hwy_obs_pe_kernel(const float* __restrict
 }
 
 // PPOMemory.compute_advantages on [T,E]: one thread per env, reversed scan over t.
-__global__ void __launch_bounds__(256) hwy_gae_kernel(const float* __restrict__ rew,
+__global__ void __launch_bounds__(64) hwy_gae_kernel(const float* __restrict__ rew,
                                                       const uint8_t* __restrict__ done,
                                                       const float* __restrict__ val,
                                                       const float* __restrict__ last_val,
@@ -1287,16 +1287,33 @@ __global__ void __launch_bounds__(256) hwy_gae_kernel(const float* __restrict__ 
   const double gl = gamma * lam;
   float last_adv = 0.0f;
   double v1 = (double)last_val[e];
-  for (int t = T - 1; t >= 0; --t) {
-    const size_t i = (size_t)t * E + e;
-    const float v0f = val[i];
-    const double nd = done[i] ? 0.0 : 1.0;
-    const double delta = ((double)rew[i] + (gamma * v1) * nd) - (double)v0f;
-    const float a = (float)(delta + (gl * nd) * (double)last_adv);
-    adv[i] = a;
-    ret[i] = a + v0f;
-    last_adv = a;
-    v1 = (double)v0f;
+  // the recurrence is sequential per env (each step rounds to float, as the reference's float
+  // tensors do), but its inputs are not: kGaeAhead steps' rewards, values and dones are loaded
+  // before they are used, so one memory round trip serves kGaeAhead steps instead of one
+  constexpr int kGaeAhead = 8;
+  for (int t1 = T; t1 > 0; t1 -= kGaeAhead) {
+    float rv[kGaeAhead], vv[kGaeAhead];
+    uint8_t dv[kGaeAhead];
+#pragma unroll
+    for (int j = 0; j < kGaeAhead; ++j) {
+      const int t = t1 - 1 - j;
+      const size_t i = (size_t)(t < 0 ? 0 : t) * E + e;
+      rv[j] = rew[i], vv[j] = val[i], dv[j] = done[i];
+    }
+#pragma unroll
+    for (int j = 0; j < kGaeAhead; ++j) {
+      const int t = t1 - 1 - j;
+      if (t < 0) break;
+      const size_t i = (size_t)t * E + e;
+      const float v0f = vv[j];
+      const double nd = dv[j] ? 0.0 : 1.0;
+      const double delta = ((double)rv[j] + (gamma * v1) * nd) - (double)v0f;
+      const float a = (float)(delta + (gl * nd) * (double)last_adv);
+      adv[i] = a;
+      ret[i] = a + v0f;
+      last_adv = a;
+      v1 = (double)v0f;
+    }
   }
 }
 
@@ -1375,8 +1392,9 @@ int hwy_launch_obs_pe(const float* in, float* out, int E, int N, int F, int kind
 int hwy_launch_gae(const float* rew, const uint8_t* done, const float* val, const float* last_val,
                    double gamma, double lam, int T, int E, float* adv, float* ret, hipStream_t s) {
   if (E == 0) return 0;
-  const int blocks = (E + 255) / 256;
-  hipLaunchKernelGGL(hwy_gae_kernel, dim3(blocks), dim3(256), 0, s, rew, done, val, last_val,
+  // one wave per workgroup: 4,096 envs spread over 64 CUs instead of 16
+  const int blocks = (E + 63) / 64;
+  hipLaunchKernelGGL(hwy_gae_kernel, dim3(blocks), dim3(64), 0, s, rew, done, val, last_val,
                      gamma, lam, T, E, adv, ret);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

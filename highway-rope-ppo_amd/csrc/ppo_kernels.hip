@@ -118,6 +118,9 @@ constexpr int kMaxRowS = 256;  // states dim bound of the fused path (LDS)
 #ifndef HWY_WG_DMA
 #define HWY_WG_DMA 1  // ppo_wgrad stages its chunks by LDS-DMA (wgrad_tile_dma); 0: register staging
 #endif
+#ifndef HWY_EARLY_GATHER
+#define HWY_EARLY_GATHER 1  // ppo_rows issues its states gather before the weight ring's prime
+#endif
 #ifndef HWY_ROWS_C64
 #define HWY_ROWS_C64 1  // 64-row ppo_rows_c tiles at H = 256 (one workgroup per CU); 0: 32-row tiles
 #endif
@@ -1146,6 +1149,37 @@ __device__ __forceinline__ void rows_out(const float* img, int pitch, float* g, 
   }
 }
 
+// The states gather of rows_forward, issued before the weight ring's first loads: vector memory
+// completes in issue order, so a gather issued after the ring's prime waited for the prime's loads
+// too.  Thread t holds elements t + i NT (row e / (Sp/4), float4 e % (Sp/4)) of the zero-padded
+// RT x Sp image; rows_forward stores them.
+template <int RT, int NT>
+struct Gathered {
+  static constexpr int N = RT * (kMaxRowS / 4) / NT;  // elements per thread at the widest S
+  f32x4 v[N];
+};
+template <int RT, int NT>
+__device__ __forceinline__ void gather_issue(const float* states, const int64_t* idx, int S,
+                                             int nrows, int row0, int H, Gathered<RT, NT>& x) {
+  int sbk, hbk;
+  rows_blocks(S, H, &sbk, &hbk);
+  const int q4 = 4 * sbk;  // Sp / 4
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < Gathered<RT, NT>::N; ++i) {
+    const int e = t + i * NT;
+    f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (e < RT * q4) {
+      const int row = e / q4, k = 4 * (e - row * q4);
+      if (row < nrows && k < S) {
+        const long src = idx ? (long)idx[row0 + row] : (long)(row0 + row);
+        v = *reinterpret_cast<const f32x4*>(states + src * S + k);
+      }
+    }
+    x.v[i] = v;
+  }
+}
+
 // Forward of the RT rows starting at row0 (rows idx[row0 + i], or row0 + i without idx) into
 // the LDS images X, H1, H2, AC = [a1 | c1]; optionally also to HBM (xg, h1, h2; null = no).
 // X may alias AC (it is dead once h1 is computed).  Ends with a workgroup barrier.
@@ -1162,7 +1196,8 @@ __device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG, TL, UN
                                              float* H1, float* H2, float* AC, float* xg,
                                              float* h1g, float* h2g, uint32_t (&mb)[2],
                                              f32x4 (&av)[RT / 16][H_TW(QH, NW)],
-                                             f32x4 (&cv)[RT / 16][H_TW(QH, NW)] PSEC_PARAMS) {
+                                             f32x4 (&cv)[RT / 16][H_TW(QH, NW)] PSEC_PARAMS,
+                                             const Gathered<RT, 64 * NW>* pre = nullptr) {
   constexpr int H = 64 * QH;
   constexpr int TW = H_TW(QH, NW);
   constexpr int NT = 64 * NW;
@@ -1183,16 +1218,30 @@ __device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG, TL, UN
   int sbk, hbk;
   rows_blocks(S, H, &sbk, &hbk);
   const int Sp = 16 * sbk, px = row_pitch(Sp);
-  // states rows, zero-padded to Sp columns and RT rows
-  for (int e = t; e < RT * (Sp / 4); e += NT) {
-    const int row = e / (Sp / 4), k = 4 * (e % (Sp / 4));
-    f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (row < nrows && k < S) {
-      const long src = idx ? (long)idx[row0 + row] : (long)(row0 + row);
-      v = *reinterpret_cast<const f32x4*>(states + src * S + k);
-      if (xg) *reinterpret_cast<f32x4*>(xg + (long)(row0 + row) * S + k) = v;
+  // states rows, zero-padded to Sp columns and RT rows (pre: gathered by gather_issue)
+  if (pre) {
+#pragma unroll
+    for (int i = 0; i < Gathered<RT, NT>::N; ++i) {
+      const int e = t + i * NT;
+      if (e < RT * (Sp / 4)) {
+        const int row = e / (Sp / 4), k = 4 * (e - row * (Sp / 4));
+        const f32x4 v = pre->v[i];
+        if (xg && row < nrows && k < S)
+          *reinterpret_cast<f32x4*>(xg + (long)(row0 + row) * S + k) = v;
+        *reinterpret_cast<f32x4*>(&X[row * px + k]) = v;
+      }
     }
-    *reinterpret_cast<f32x4*>(&X[row * px + k]) = v;
+  } else {
+    for (int e = t; e < RT * (Sp / 4); e += NT) {
+      const int row = e / (Sp / 4), k = 4 * (e % (Sp / 4));
+      f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (row < nrows && k < S) {
+        const long src = idx ? (long)idx[row0 + row] : (long)(row0 + row);
+        v = *reinterpret_cast<const f32x4*>(states + src * S + k);
+        if (xg) *reinterpret_cast<f32x4*>(xg + (long)(row0 + row) * S + k) = v;
+      }
+      *reinterpret_cast<f32x4*>(&X[row * px + k]) = v;
+    }
   }
   __syncthreads();
   PSEC(0);
@@ -1277,22 +1326,24 @@ __device__ __forceinline__ void rows_body(const RowArgs& r) {
   constexpr int D = CMP ? HWY_RING_DC : ring_depth<TW>();  // CMP: 4 waves per SIMD hide more
   WRing<TW, D, 7, true, CMP> R;
   ring_setup(R, P, r.off, S, H, w * (H / NW), r.tiles);
+  // the loss head's inputs and weights, loaded now so that their latency hides behind the
+  // forward: lane l < RPW of wave w holds row RPW*w + l; the head weights of this wave's
+  // output columns nb + 16t + (lane & 15).  HWY_EARLY_GATHER: the row indices of the head and of
+  // the states gather go out first, then the rows they name, then the weight ring's prime
+  // (vector memory completes in issue order: a gather behind the prime waited for it)
+  const int hl = min(RPW * w + min(lane, RPW - 1), nrows - 1);
+  float hz0, hz1, hold, hadv, hret;
+  const long hsrc = (long)r.idx[row0 + hl];
+  Gathered<RT, NT> xpre;
+  if constexpr (HWY_EARLY_GATHER) gather_issue<RT, NT>(r.states, r.idx, S, nrows, row0, H, xpre);
+  hz0 = r.pre_tanh[hsrc * 2];
+  hz1 = r.pre_tanh[hsrc * 2 + 1];
+  hold = r.old_logp[hsrc];
+  hadv = r.adv[hsrc];
+  hret = r.ret[hsrc];
   R.prime();
   const int nb = w * (H / NW);  // this wave's output columns of an H-wide layer
   f32x4 acc[RB][TW];
-  // the loss head's inputs and weights, loaded now so that their latency hides behind the
-  // forward: lane l < RPW of wave w holds row RPW*w + l; the head weights of this wave's
-  // output columns nb + 16t + (lane & 15)
-  const int hl = min(RPW * w + min(lane, RPW - 1), nrows - 1);
-  float hz0, hz1, hold, hadv, hret;
-  {
-    const long src = (long)r.idx[row0 + hl];
-    hz0 = r.pre_tanh[src * 2];
-    hz1 = r.pre_tanh[src * 2 + 1];
-    hold = r.old_logp[src];
-    hadv = r.adv[src];
-    hret = r.ret[src];
-  }
   // the squash correction depends on the stored pre-tanh actions only: computed here, its
   // latency hides behind the forward instead of lengthening the loss head's dependent chain
   const float hq0 = log1pf(-(tanhf(hz0) * tanhf(hz0)) + 1e-6f);
@@ -1311,7 +1362,7 @@ __device__ __forceinline__ void rows_body(const RowArgs& r) {
   uint32_t mb[2] = {0u, 0u};      // CMP: ReLU decisions of h1, h2 (this lane's C elements)
   rows_forward<QH, NW, RT, true, D, 7, true, CMP>(R, r.states, r.idx, S, nrows, row0, P, r.off, X,
                                                   H1, P1, AC, r.xg, r.h1, r.h2, mb, av,
-                                                  cv PSEC_ARGS);
+                                                  cv PSEC_ARGS, HWY_EARLY_GATHER ? &xpre : nullptr);
   PSEC(3);
   const int g4 = lane >> 4, c16 = lane & 15;
 
@@ -1618,6 +1669,9 @@ ppo_act_c(ActArgs r) {
   constexpr int D = HWY_RING_DC;
   WRing<TW, D, 4, true, true> R;
   ring_setup(R, P, r.off, r.S, H, w * (H / NW), r.tiles);
+  Gathered<RT, 64 * NW> xpre;  // the states rows, issued before the ring's prime (rows_body)
+  if constexpr (HWY_EARLY_GATHER)
+    gather_issue<RT, 64 * NW>(r.states, nullptr, r.S, nrows, row0, H, xpre);
   R.prime();
 #ifdef HWY_SECTION_PROFILE
   uint64_t _pt = 0, _pacc[16];
@@ -1642,7 +1696,8 @@ ppo_act_c(ActArgs r) {
   uint32_t mb[2] = {0u, 0u};
   rows_forward<QH, NW, RT, true, D, 4, true, false>(R, r.states, nullptr, r.S, nrows, row0, P,
                                                      r.off, P1, H1, P1, nullptr, nullptr,
-                                                     nullptr, nullptr, mb, av, cv PSEC_ARGS);
+                                                     nullptr, nullptr, mb, av, cv PSEC_ARGS,
+                                                     HWY_EARLY_GATHER ? &xpre : nullptr);
   const int g4 = lane >> 4, c16 = lane & 15;
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
@@ -2572,15 +2627,18 @@ constexpr int kAdamEPT = HWY_ADAM_EPT;  // elements per thread (same box: 1 5.9 
 
 // clip_grad_norm_'s coefficient from the norm partials and Adam's bias corrections, into
 // sh[0] (coef), sh[1] (lr / bc1), sh[2] (sqrt bc2); every thread of the workgroup calls it
-__device__ __forceinline__ void adam_scalars(const OptArgs& o, float* red, float* sh) {
+// first / t: this thread's first norm partial (norm_part[threadIdx.x], 0 past nred) and the Adam
+// step, loaded by the caller ahead of its other loads (vector memory completes in issue order)
+__device__ __forceinline__ void adam_scalars(const OptArgs& o, float* red, float* sh, float first,
+                                             int t) {
   float s = 0.0f;
-  for (int k = threadIdx.x; k < o.nred; k += 256) s += o.norm_part[k];
+  if ((int)threadIdx.x < o.nred) s += first;
+  for (int k = threadIdx.x + 256; k < o.nred; k += 256) s += o.norm_part[k];
   s = wave_sum_dpp(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   if (threadIdx.x == 64) {  // wave 1, while the norm partials combine
     // torch.optim.Adam (foreach, non-capturable): bias corrections in double on the host side
     // (beta ** t by binary powering: a few dependent multiplies instead of a double pow())
-    const int t = o.counters[0];
     double p1 = 1.0, p2 = 1.0, b1 = (double)o.beta1, b2 = (double)o.beta2;
     for (int e = t; e > 0; e >>= 1) {
       if (e & 1) p1 *= b1, p2 *= b2;
@@ -2619,8 +2677,10 @@ __device__ __forceinline__ void adam_elem(const OptArgs& o, int64_t i, float g_r
 __global__ void __launch_bounds__(256) ppo_adam(OptArgs o) {
   __shared__ float red[4];
   __shared__ float sh[3];
-  // this thread's elements first (256 apart, coalesced): their loads overlap the norm
-  // reduction's
+  // the norm partial and the step count first (the clip coefficient's chain waits on them), then
+  // this thread's elements (256 apart, coalesced), whose loads overlap the norm reduction
+  const float first = (int)threadIdx.x < o.nred ? o.norm_part[threadIdx.x] : 0.0f;
+  const int step = o.counters[0];
   float g_raw[kAdamEPT], m_old[kAdamEPT], v_old[kAdamEPT], p_old[kAdamEPT];
 #pragma unroll
   for (int q = 0; q < kAdamEPT; ++q) {
@@ -2628,7 +2688,7 @@ __global__ void __launch_bounds__(256) ppo_adam(OptArgs o) {
     const int64_t ii = i < o.numel ? i : 0;
     g_raw[q] = o.grads[ii], m_old[q] = o.m[ii], v_old[q] = o.v[ii], p_old[q] = o.params[ii];
   }
-  adam_scalars(o, red, sh);
+  adam_scalars(o, red, sh, first, step);
 #pragma unroll
   for (int q = 0; q < kAdamEPT; ++q) {
     const int64_t i = ((int64_t)blockIdx.x * kAdamEPT + q) * 256 + threadIdx.x;
