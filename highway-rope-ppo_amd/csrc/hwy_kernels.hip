@@ -26,7 +26,9 @@
 #include "hwy_internal.h"
 
 #define WAVE 64
-#define ENVS_PER_BLOCK 4
+#ifndef ENVS_PER_BLOCK
+#define ENVS_PER_BLOCK 4  // envs (one wave each) per workgroup
+#endif
 
 // upstream constants (same literals as oracle/hwy_oracle.c)
 #define LANE_WIDTH 4.0f
