@@ -3,6 +3,7 @@
 // -- at 1, 2 and 4 waves per SIMD, with operands (a) in registers, (b) A from LDS (ds_read_b128
 // one block ahead) and B from a global ring (global_load_dwordx4, 2 blocks ahead) as ppo_rows_c
 // streams them.  Prints TFLOP/s and the fraction of the 157.3 TF/s fp32 MFMA peak.
+// Build: hipcc --offload-arch=gfx950 -O3 tools/micro/mfma_f32_rate.hip -o tools/micro/mfma_f32_rate
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
