@@ -26,9 +26,8 @@
 #include "hwy_internal.h"
 
 #define WAVE 64
-#ifndef ENVS_PER_BLOCK
-#define ENVS_PER_BLOCK 4  // envs (one wave each) per workgroup
-#endif
+// envs (one wave each) per workgroup: 1, 2 and 4 measured the same (round 4)
+constexpr int ENVS_PER_BLOCK = 4;
 
 // upstream constants (same literals as oracle/hwy_oracle.c)
 #define LANE_WIDTH 4.0f
@@ -176,12 +175,13 @@ __device__ unsigned long long g_hwy_wave_t[5 * HWY_NWT];
 #define WAVE_HWID() 0ull
 #endif
 
-// Development pricing builds only (make variant VEXTRA=-DHWY_SKIP=mask; WRONG results, never the
-// product): skip one part of the frame to price its instruction count (tools/ab.sh MODE=pmc).
-// 1 MOBIL, 2 the SAT pair loop, 4 collision candidates + SAT, 8 the abort loop, 16 steering,
-// 32 the IDM pow, 64 the observation's rank count
-#ifndef HWY_SKIP
-#define HWY_SKIP 0
+// Development pricing builds only (hwy_dev_knobs.h, a make variant with -DHWY_DEV_KNOBS and the
+// mask; WRONG results, never the product): kSkip skips parts of the frame to price their
+// instruction count.  The product build compiles every such site away (kSkip = 0).
+#ifdef HWY_DEV_KNOBS
+#include "hwy_dev_knobs.h"
+#else
+constexpr int kSkip = 0;
 #endif
 
 // ------------------------------------------------------------------------- vehicle state
@@ -228,7 +228,7 @@ __device__ __forceinline__ float desired_gap(float a_spd, float a_c, float a_s, 
 __device__ __forceinline__ float idm_free(float ev_spd, float ev_tsp, float delta, float limit) {
   float tsp = hm_clipf(ev_tsp, 0.0f, limit);
   float base = hm_maxf(ev_spd, 0.0f) / hm_absf(hm_not_zero(tsp));
-  if (HWY_SKIP & 32) return hm_fma(-COMFORT_ACC_MAX, base * base, COMFORT_ACC_MAX);
+  if (kSkip & 32) return hm_fma(-COMFORT_ACC_MAX, base * base, COMFORT_ACC_MAX);
   return hm_fma(-COMFORT_ACC_MAX, hm_powf(base, delta), COMFORT_ACC_MAX);
 }
 
@@ -492,7 +492,7 @@ __device__ void observe_wave(const hwy_config& C, int lane, const Veh& v, float 
               (C.see_behind || -2.0f * VEH_LENGTH < v.x - ex);
   const uint64_t em = ballot(elig);
   int rank;
-  if (C.order == HWY_ORDER_SORTED && (HWY_SKIP & 64)) {
+  if (C.order == HWY_ORDER_SORTED && (kSkip & 64)) {
     rank = __popcll(em & ((1ull << lane) - 1ull));
   } else if (C.order == HWY_ORDER_SORTED) {
     float key = hm_absf(v.x - ex);
@@ -880,7 +880,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   SEC(sp, 2);
   int ntl = v.tl;
   bool gain[2] = {false, false};
-  if (fire && !(HWY_SKIP & 1)) {
+  if (fire && !(kSkip & 1)) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int c = v.ln - 1 + 2 * q;
@@ -927,7 +927,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   // abort an ongoing lane change if another car targets the same lane within its desired gap,
   // in road order (lower indices already final, higher ones at their frame-start target)
   int tl_cur = ntl;
-  uint64_t cm = (HWY_SKIP & 8) ? 0ull : ballot(actor && mid);
+  uint64_t cm = (kSkip & 8) ? 0ull : ballot(actor && mid);
   // a lane can trigger an abort only while its visible target is not its own lane (vis == tj
   // and ln != tj), under either visibility; aborts only ever clear that, so this superset holds
   // for the whole loop
@@ -964,7 +964,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   const float ft_x = shf(v.x, st_), ft_spd = shf(v.spd, st_), ft_c = shf(ch, st_),
               ft_s = shf(sh, st_);
   if (actor) {
-    const float steer = (HWY_SKIP & 16) ? 0.0f : steering_tan(v.y, v.h, v.spd, v.tl);
+    const float steer = (kSkip & 16) ? 0.0f : steering_tan(v.y, v.h, v.spd, v.tl);
     float acc = self_a;
     if (need_t) {
       const float acc_t =
@@ -1039,7 +1039,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
     const float xs = shf(v.x, ro.ord);  // x at position `lane`
     float xu = xs;
     bool up = lane < npres;
-    if (HWY_SKIP & 4) up = false;
+    if (kSkip & 4) up = false;
     for (int o = 1; wave_any(up); ++o) {
       xu = __int_as_float(shl1i(__float_as_int(xu)));  // x at position lane + o
       up = up && lane + o < npres && !(hm_absf(xu - xs) > xbound);
@@ -1069,7 +1069,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
     cl.plist[off++] = (uint16_t)((lo << 8) | hi);
   }
   wave_lds_sync();
-  for (int base = 0; base < ((HWY_SKIP & 2) ? 0 : total); base += WAVE) {
+  for (int base = 0; base < ((kSkip & 2) ? 0 : total); base += WAVE) {
     const bool has = base + lane < total;
     const int pr = has ? cl.plist[base + lane] : 0;
     const int a = pr >> 8, b = pr & 0xff;  // a < b
@@ -1347,9 +1347,8 @@ __global__ void hwy_math_kernel(int op, const float* in, const float* in2, float
 // ------------------------------------------------------------------------- launch helpers
 extern "C" {
 // compute units of the current device (cached per device; 256 without one)
-#ifndef HWY_STEP_BIG_W
-#define HWY_STEP_BIG_W 6  // waves per SIMD the step kernel's registers are sized for at large E
-#endif
+// waves per SIMD the step kernel's registers are sized for at large E (5 and 8 measured slower)
+constexpr int kStepBigW = 6;
 static int device_cus() {
   static int cache[64] = {};
   int dev = 0;
@@ -1372,7 +1371,7 @@ int hwy_launch_step(const StepParams* p, hipStream_t s) {
   const int blocks = (p->cfg.num_envs + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
   // one wave per env: more than 4 waves per SIMD of envs queue behind the first four
   if ((int64_t)p->cfg.num_envs > (int64_t)16 * device_cus())
-    hipLaunchKernelGGL(hwy_step_kernel<HWY_STEP_BIG_W>, dim3(blocks), dim3(ENVS_PER_BLOCK * WAVE), 0, s, *p);
+    hipLaunchKernelGGL(hwy_step_kernel<kStepBigW>, dim3(blocks), dim3(ENVS_PER_BLOCK * WAVE), 0, s, *p);
   else
     hipLaunchKernelGGL(hwy_step_kernel<4>, dim3(blocks), dim3(ENVS_PER_BLOCK * WAVE), 0, s, *p);
   return hipGetLastError() == hipSuccess ? 0 : -1;

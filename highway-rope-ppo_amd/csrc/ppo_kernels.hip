@@ -103,48 +103,17 @@ constexpr int kKStep = 32;
 constexpr int kHeadRows = 16;  // minibatch rows per head workgroup (4 per wave)
 constexpr int kRowTile = 16;   // minibatch rows per ppo_rows workgroup
 constexpr int kMaxRowS = 256;  // states dim bound of the fused path (LDS)
-#ifndef HWY_ROWS_NW
-#define HWY_ROWS_NW 8  // ppo_rows waves at H = 256 (16: 4 per SIMD, one 16-column tile each)
-#endif
-#ifndef HWY_ROWS_CMP
-#define HWY_ROWS_CMP 1  // ppo_rows' compact LDS at H = 256, 32-row tiles (two workgroups per CU)
-#endif
-#ifndef HWY_WG_EXP
-// timing-only ppo_wgrad experiments (wrong results; development builds): 1 no LDS staging, 2 no
-// global loads after the first chunk, 3 no barriers in the chunk loop, 4 no MFMAs, 5 (LDS-DMA
-// loop) no B-operand loads
-#define HWY_WG_EXP 0
-#endif
-#ifndef HWY_WG_DMA
-#define HWY_WG_DMA 1  // ppo_wgrad stages its chunks by LDS-DMA (wgrad_tile_dma); 0: register staging
-#endif
-#ifndef HWY_EARLY_GATHER
-#define HWY_EARLY_GATHER 1  // ppo_rows issues its states gather before the weight ring's prime
-#endif
-#ifndef HWY_ROWS_C64
-#define HWY_ROWS_C64 1  // 64-row ppo_rows_c tiles at H = 256 (one workgroup per CU); 0: 32-row tiles
-#endif
-#ifndef HWY_WG_TEAMS
-#define HWY_WG_TEAMS 0  // 1: ppo_wgrad's row halves sync on LDS counters, not the chunk barrier
-#endif
-#ifndef HWY_WG_SPREAD
-// 1 (default): ppo_wgrad's LDS-DMA pieces for chunk c + 2 go out between chunk c's MFMA groups
-// instead of all six right after the barrier, where both waves of a SIMD issued them at once
-// (round 4: with HWY_RING_RA 203.4 -> 201.5 us per 16,384-row step, bit-identical weights)
-#define HWY_WG_SPREAD 1
-#endif
-#ifndef HWY_RING_RA
-// 1 (default): the row kernels' activation reads pinned one block ahead of their MFMAs (the
-// scheduler had sunk them to the end of the previous block, so every block opened on an LDS
-// wait); measured alone 203.4 -> 201.4 us per 16,384-row step, bit-identical weights
-#define HWY_RING_RA 1
-#endif
-#ifndef HWY_RING_DC
-#define HWY_RING_DC 2  // weight blocks in flight per wave in the compact-LDS ppo_rows
-#endif
-#ifndef HWY_ROWS_NW32
-#define HWY_ROWS_NW32 8  // the same for the 32-row tiles
-#endif
+// Product constants, each measured against its alternatives (the rejected
+// alternatives are in git history, round 4 and earlier):
+//  - ppo_rows at H = 256, 16-row tiles: 8 waves (2 per SIMD, two 16-column tiles each);
+//  - 32-row tiles at H = 256: the compact-LDS ppo_rows_c (two workgroups per CU), 8 waves;
+//  - 64-row tiles at H = 256 once every CU gets one (ppo_rows_c64, one workgroup per CU);
+//  - the row kernels issue their states gather before the weight ring's prime (vector memory
+//    completes in issue order) and pin their activation reads one block ahead of the MFMAs;
+//  - ppo_wgrad stages its chunks by LDS-DMA, the next chunk's pieces spread between the MFMA
+//    groups of the current one;
+//  - kRingDC weight blocks in flight per wave in the compact-LDS row kernels.
+constexpr int kRingDC = 2;
 constexpr int kWgTM = 128, kWgTN = 64;          // ppo_wgrad output tile
 constexpr int kWgWaves = 8;                     // ppo_wgrad waves (2 per SIMD)
 constexpr int kWgPart = kWgTM * kWgTN + kWgTM;  // floats per partial tile (+ bias sums)
@@ -433,12 +402,9 @@ __host__ __device__ inline TileGeom tile_geom(int S, int H, int sb, int hb) {
   return T;
 }
 // ring depth of the row kernels for H (ppo_rows<H/64, NW>: 16-column tiles per wave TW)
-#ifndef HWY_RING_D2
-#define HWY_RING_D2 4  // weight blocks in flight per wave when a wave owns <= 2 column tiles
-#endif
 __host__ __device__ inline int rows_ring_depth(int H) {
   const int qh = H / 64, nw = (qh % 2 == 0) ? 8 : 4, tw = H / nw / 16;
-  return tw <= 2 ? HWY_RING_D2 : (tw <= 4 ? 4 : 2);
+  return tw <= 4 ? 4 : 2;  // weight blocks in flight per wave
 }
 __host__ __device__ inline void rows_blocks(int S, int H, int* sb, int* hb) {
   const int D = rows_ring_depth(H);
@@ -552,9 +518,9 @@ inline int rows_tile(int B, int H) {
   if (H > 256) return kRowTile;
   // 64-row tiles (ppo_rows_c64, one workgroup per CU) once every CU gets one: each weight
   // fragment then feeds 4 row blocks, half the weight loads per MFMA of the 32-row tiles
-  if (HWY_ROWS_C64 && H == 256 && B >= 64 * chip_geom().cus) return 4 * kRowTile;
-  const int force = dev_knob_int("HWY_ROWS_RT", 0);
+  const int force = dev_knob_int("HWY_ROWS_RT", 0);  // development builds only
   if (force == 16 || force == 32) return force;
+  if (H == 256 && B >= 64 * chip_geom().cus) return 4 * kRowTile;
   return B >= 32 * chip_geom().cus ? 2 * kRowTile : kRowTile;
 }
 
@@ -955,11 +921,9 @@ struct WRing {
           a[rb] = a_nxt[rb];
           a_nxt[rb] = *reinterpret_cast<const f32x4*>(arow + 16 * rb * pa + kn);
         }
-#if HWY_RING_RA
         // pinned: the next block's activation reads go out before this block's MFMAs (the
         // scheduler otherwise sinks them to the block's end, right before their use)
         __builtin_amdgcn_sched_barrier(0);
-#endif
         const bool kin = kb + 4 * g < sg[SEG].K;  // else the block was clamped: weights are 0
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -988,7 +952,7 @@ __device__ __forceinline__ void zero_acc(f32x4 (&acc)[RB][TW]) {
 }
 
 template <int TW>
-constexpr int ring_depth() { return TW <= 2 ? HWY_RING_D2 : (TW <= 4 ? 4 : 2); }
+constexpr int ring_depth() { return TW <= 4 ? 4 : 2; }
 
 // segment table of the row kernels: forward W1, W2, Wa1, Wc1 ([N][K]); backward Wa1, Wc1, W2
 // read k-major for dh2 = dac [Wa1; Wc1] and dh1 = dh2 W2.  With a tile image (TileGeom; kept by
@@ -1323,19 +1287,19 @@ __device__ __forceinline__ void rows_body(const RowArgs& r) {
   const int row0 = blockIdx.x * RT;
   const int nrows = min(RT, r.B - row0);
   const float* P = r.params;
-  constexpr int D = CMP ? HWY_RING_DC : ring_depth<TW>();  // CMP: 4 waves per SIMD hide more
+  constexpr int D = CMP ? kRingDC : ring_depth<TW>();  // CMP: 4 waves per SIMD hide more
   WRing<TW, D, 7, true, CMP> R;
   ring_setup(R, P, r.off, S, H, w * (H / NW), r.tiles);
   // the loss head's inputs and weights, loaded now so that their latency hides behind the
   // forward: lane l < RPW of wave w holds row RPW*w + l; the head weights of this wave's
-  // output columns nb + 16t + (lane & 15).  HWY_EARLY_GATHER: the row indices of the head and of
+  // output columns nb + 16t + (lane & 15).  The row indices of the head and of
   // the states gather go out first, then the rows they name, then the weight ring's prime
   // (vector memory completes in issue order: a gather behind the prime waited for it)
   const int hl = min(RPW * w + min(lane, RPW - 1), nrows - 1);
   float hz0, hz1, hold, hadv, hret;
   const long hsrc = (long)r.idx[row0 + hl];
   Gathered<RT, NT> xpre;
-  if constexpr (HWY_EARLY_GATHER) gather_issue<RT, NT>(r.states, r.idx, S, nrows, row0, H, xpre);
+  gather_issue<RT, NT>(r.states, r.idx, S, nrows, row0, H, xpre);
   hz0 = r.pre_tanh[hsrc * 2];
   hz1 = r.pre_tanh[hsrc * 2 + 1];
   hold = r.old_logp[hsrc];
@@ -1362,7 +1326,7 @@ __device__ __forceinline__ void rows_body(const RowArgs& r) {
   uint32_t mb[2] = {0u, 0u};      // CMP: ReLU decisions of h1, h2 (this lane's C elements)
   rows_forward<QH, NW, RT, true, D, 7, true, CMP>(R, r.states, r.idx, S, nrows, row0, P, r.off, X,
                                                   H1, P1, AC, r.xg, r.h1, r.h2, mb, av,
-                                                  cv PSEC_ARGS, HWY_EARLY_GATHER ? &xpre : nullptr);
+                                                  cv PSEC_ARGS, &xpre);
   PSEC(3);
   const int g4 = lane >> 4, c16 = lane & 15;
 
@@ -1561,12 +1525,6 @@ struct ActArgs {
   const float* tiles;  // weight tile image in step with params (TL), else null
 };
 
-#ifndef HWY_ACT_CMP
-#define HWY_ACT_CMP 1  // ppo_act_c at H = 256 from the tile image (0: always ppo_act)
-#endif
-#ifndef HWY_ACT_NW
-#define HWY_ACT_NW 8  // waves of ppo_act at H = 256 (development A/B)
-#endif
 template <int QH, int NW, bool TL>
 __global__ void __launch_bounds__(64 * NW, 1) ppo_act(ActArgs r) {
   constexpr int H = 64 * QH;
@@ -1666,12 +1624,11 @@ ppo_act_c(ActArgs r) {
   const int row0 = blockIdx.x * RT;
   const int nrows = min(RT, r.B - row0);
   const float* P = r.params;
-  constexpr int D = HWY_RING_DC;
+  constexpr int D = kRingDC;
   WRing<TW, D, 4, true, true> R;
   ring_setup(R, P, r.off, r.S, H, w * (H / NW), r.tiles);
   Gathered<RT, 64 * NW> xpre;  // the states rows, issued before the ring's prime (rows_body)
-  if constexpr (HWY_EARLY_GATHER)
-    gather_issue<RT, 64 * NW>(r.states, nullptr, r.S, nrows, row0, H, xpre);
+  gather_issue<RT, 64 * NW>(r.states, nullptr, r.S, nrows, row0, H, xpre);
   R.prime();
 #ifdef HWY_SECTION_PROFILE
   uint64_t _pt = 0, _pacc[16];
@@ -1697,7 +1654,7 @@ ppo_act_c(ActArgs r) {
   rows_forward<QH, NW, RT, true, D, 4, true, false>(R, r.states, nullptr, r.S, nrows, row0, P,
                                                      r.off, P1, H1, P1, nullptr, nullptr,
                                                      nullptr, nullptr, mb, av, cv PSEC_ARGS,
-                                                     HWY_EARLY_GATHER ? &xpre : nullptr);
+                                                     &xpre);
   const int g4 = lane >> 4, c16 = lane & 15;
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
@@ -1751,21 +1708,13 @@ ppo_act_c(ActArgs r) {
 // dW1 = dh1^T gather(states)).  Workgroup id = tile * split + z: slice z of the minibatch rows
 // (B / split rows, split = 8 at the bench shapes) goes to workgroup id % 8 = the XCD the
 // dispatcher places it on, so each XCD reads one 1/8 row slice (~3 MB at B = 4096, H = 256) and
-// keeps it in its own L2 across all the tiles.  One workgroup per CU (96 KB LDS), 4 waves; each
-// wave accumulates a 64 x 32 block as two 32x32 v_mfma_f32_32x32x2_f32 accumulators that share
-// the B operand.
+// keeps it in its own L2 across all the tiles.  One 512-thread workgroup per CU (8 waves, 2 per
+// SIMD); the two waves of a SIMD own the same 64 x 32 output block as two 32x32
+// v_mfma_f32_32x32x2_f32 accumulators sharing the B operand, over the two row halves of every
+// 64-row chunk (summed through LDS at the end).  The chunks are staged by LDS-DMA
+// (wgrad_tile_dma: three buffers, two chunks in flight).
 //
-// K (the minibatch rows) runs in 64-row chunks staged through LDS as [feature][row] images: each
-// thread loads 4 rows x 4 features (four float4 row segments, coalesced), transposes them in
-// registers and stores 4 float4 row-quads.  In the MFMA loop lane (l32, h) reads the float4 of
-// rows 8G + 4h .. 8G + 4h + 3 of its feature, one ds_read_b128 per 4 MFMA steps; k-step j of
-// group G then sums rows 8G + j and 8G + 4 + j (a permutation of the chunk, which the sum does
-// not see).  Quad q of feature row m is stored at slot q ^ wg_swz(m): conflict-free for both the
-// transposing ds_write_b128 (8-lane groups, m = 4c + i) and the ds_read_b128 (16-lane groups).
-//
-// The next chunk's global loads are issued before a chunk's MFMAs and its transposing LDS stores
-// are interleaved into them (two selects per MFMA), so one wave per SIMD keeps the matrix pipe
-// busy.  The split partial tiles go to a slab that ppo_wsum sums in split order (the kernel
+// The split partial tiles go to a slab that ppo_wsum sums in split order (the kernel
 // boundary is the one L2 writeback that makes the other XCDs' partials visible; a last-arriver
 // reduction inside this kernel paid an agent-scope L2 writeback per workgroup, ~20 us).
 struct WgArgs {
@@ -1798,13 +1747,6 @@ __device__ __forceinline__ float block_sum4(float v, float* red) {
   for (int i = 1; i < NW; ++i) s += red[i];
   return s;
 }
-
-// slot swizzle of an LDS image with 64-float feature rows (16 row-quads): bijective in m >> 2
-// mod 8 for each m & 3 (the store groups) and in m mod 16 over every ds_read_b128 lane group
-__device__ __forceinline__ int wg_swz(int m) {
-  return (((m >> 2) ^ ((m & 3) >> 1)) & 7) | ((m & 1) << 3);
-}
-__device__ __forceinline__ int wg_at(int m, int q) { return m * 64 + 4 * (q ^ wg_swz(m)); }
 
 // head parameters (the ppo_rows partials summed in row-block order) + the metrics row
 __device__ void wgrad_head(const WgArgs& a, int hid, float* lds, float* red) {
@@ -1872,7 +1814,7 @@ __device__ void wgrad_head(const WgArgs& a, int hid, float* lds, float* red) {
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-// ppo_wgrad's chunk loop with LDS-DMA staging (HWY_WG_DMA, the default).  Chunks of 64 rows go
+// ppo_wgrad's chunk loop with LDS-DMA staging.  Chunks of 64 rows go
 // global -> LDS by global_load_lds_dwordx4 (1 KB per wave instruction, no VGPRs, no VALU) into
 // row-major images: A = 64 rows x 128 features (32 pieces of 2 rows), B = 64 rows x 64 features
 // (16 pieces of 4 rows); each wave issues 4 A and 2 B pieces per chunk.  Odd rows are stored
@@ -1884,7 +1826,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 // barrier (counted vmcnt, raw s_barrier).  The register-staged loop spent 14 us of a 75 us
 // launch in its transposing staging (timing-only build without it: 61 us).
 // The A column sums (bias gradients) come from the A operand values in registers.
-[[maybe_unused]] __device__ __forceinline__ void wgrad_tile_dma(const WgArgs& a, int tile_id, int kb0, int kb1,
+__device__ __forceinline__ void wgrad_tile_dma(const WgArgs& a, int tile_id, int kb0, int kb1,
                                                float* part, float* wg_lds PSEC_PARAMS) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, l32 = lane & 31;
   const int H = a.H;
@@ -1929,7 +1871,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
                                        (lds_void_t*)(buf + (4 * w + i) * 256), 16, 0, 0);
     }
 #pragma unroll
-    for (int i = 0; i < (HWY_WG_EXP == 5 ? 0 : 2); ++i) {
+    for (int i = 0; i < 2; ++i) {
       if (part >= 0 && part != 2) continue;
       const uint32_t row = (uint32_t)min(k0 + 4 * (2 * w + i) + rb, kb1 - 1);
       __builtin_amdgcn_global_load_lds((const void*)(Bm + (row * (uint32_t)ldb + b_col)),
@@ -1949,8 +1891,9 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 #pragma unroll
   for (int q = 0; q < 16; ++q) acc0[q] = acc1[q] = 0.0f;
   float bs0 = 0.0f, bs1 = 0.0f;  // A column sums of this lane's features over its rows
-  // dc / dbuf: the chunk whose DMAs go out between this chunk's MFMA groups (HWY_WG_SPREAD;
-  // dc < 0: none)
+  // dc / dbuf: the chunk whose DMAs go out between this chunk's MFMA groups (dc < 0: none);
+  // issued all at once after the barrier, both waves of a SIMD issued them together (round 4:
+  // 203.4 -> 201.5 us per 16,384-row step with the activation reads pinned, same weights)
   auto compute = [&](const float* buf, int lim, auto mask_tag, int dc, float* dbuf) {
     constexpr bool MASK = decltype(mask_tag)::value;  // rows >= lim (of the chunk) are zero
     const float* pa0 = buf + offa0 + 32 * kh * 128;
@@ -1988,7 +1931,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
         acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(u1, y[b][j], acc1, 0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (HWY_WG_SPREAD && g < 3 && dc >= 0) {
+      if (g < 3 && dc >= 0) {
         dma(dc, dbuf, g);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -1999,15 +1942,6 @@ typedef __attribute__((address_space(3))) void lds_void_t;
   float* b0 = wg_lds;
   float* b1 = wg_lds + BUF;
   float* b2 = wg_lds + 2 * BUF;
-  // HWY_WG_TEAMS: the two row halves of a chunk (waves 0-3: rows 0-31, waves 4-7: rows 32-63)
-  // touch disjoint LDS rows -- each half DMAs, and reads, only its own -- so each half
-  // synchronises on its own arrival counter in LDS instead of the workgroup barrier, and the two
-  // waves of a SIMD (one per half) drift out of step instead of meeting at every chunk's barrier
-  int* const team_cnt = reinterpret_cast<int*>(wg_lds + 3 * (kWgTM + kWgTN) * 64 + kWgWaves);
-  if (HWY_WG_TEAMS) {
-    if (t < 2) team_cnt[t] = 0;
-    __syncthreads();
-  }
   // earlier stores of this wave (a previous tile's partial) drained: the vmcnt counts are exact
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   dma(0, b0);
@@ -2015,33 +1949,13 @@ typedef __attribute__((address_space(3))) void lds_void_t;
   auto step = [&](int c, auto mask_tag) {
     // this wave's pieces of chunk c landed (chunk c + 1's 6 may still be in flight) and its
     // reads of chunk c - 1 returned; after the barrier, every wave's
-    if (c + 1 < nchunk && HWY_WG_EXP == 5)
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if (c + 1 < nchunk)
+    if (c + 1 < nchunk)
       asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (HWY_WG_TEAMS) {
-      // arrive (this wave's DMA of chunk c has landed and its reads of chunk c - 1 returned),
-      // then wait for the other three waves of the half: every chunk raises the count by 4
-      // (inline asm: as C++ atomics the compiler orders them behind every LDS-DMA in flight,
-      // s_waitcnt vmcnt(0), which would drain chunk c + 1's prefetch)
-      const uint32_t ca = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int*)(team_cnt + kh);
-      if (lane == 0) asm volatile("ds_add_u32 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"(ca), "v"(1) : "memory");
-      const int target = 4 * (c + 1);
-      for (;;) {
-        int seen;
-        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(seen) : "v"(ca) : "memory");
-        if (__builtin_amdgcn_readfirstlane(seen) >= target) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    } else {
-      __builtin_amdgcn_s_barrier();
-    }
-    // chunk c + 2 into chunk c - 1's buffer: here, or spread between this chunk's MFMA groups
-    if (!HWY_WG_SPREAD && c + 2 < nchunk) dma(c + 2, b2);
+    __builtin_amdgcn_s_barrier();
+    // chunk c + 2 into chunk c - 1's buffer, spread between this chunk's MFMA groups
     compute(b0, kb1 - (kb0 + 64 * c), mask_tag, c + 2 < nchunk ? c + 2 : -1, b2);
     float* tb = b0;
     b0 = b1, b1 = b2, b2 = tb;
@@ -2086,205 +2000,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
   PSEC(9);
 }
 
-// Rows [kb0, kb1) of output tile tile_id into the partial tile `part` (+ the bias column sums
-// when the tile owns a bias column); an empty range writes a zero partial.
-[[maybe_unused]] __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int tile_id, int kb0, int kb1,
-                                           float* part, float* wg_lds PSEC_PARAMS) {
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, l32 = lane & 31;
-  const int H = a.H;
-  if (kb1 <= kb0) {
-    for (int i = t; i < kWgPart; i += 64 * kWgWaves) part[i] = 0.0f;
-    return;
-  }
-  int id = tile_id;
-  const float *A, *Bm;
-  int lda, ldb, M, N, ntj;
-  if (id < a.tac) {  // dWac = dac^T h2
-    A = a.dac, lda = 2 * H, Bm = a.h2, ldb = H, M = 2 * H, N = H;
-  } else if (id < a.tac + a.t2) {  // dW2 = dh2^T h1
-    id -= a.tac;
-    A = a.dh2, lda = H, Bm = a.h1, ldb = H, M = H, N = H;
-  } else {  // dW1 = dh1^T x (gathered states rows written by ppo_rows)
-    id -= a.tac + a.t2;
-    A = a.dh1, lda = H, Bm = a.xg, ldb = a.S, M = H, N = a.S;
-  }
-  ntj = (N + kWgTN - 1) / kWgTN;
-  const int ti = id / ntj, tj = id % ntj;
-  const int i0 = ti * kWgTM, j0 = tj * kWgTN;
-  const int nchunk = (kb1 - kb0 + 63) / 64;  // >= 1
-
-  // staging (64-row chunks): A = 64 rows x 128 features, thread: features 4ca .. 4ca+3 of rows
-  // 8w + 4ra .. +3; B = 64 rows x 64 features, waves 0-3, thread: features 4cb.. of rows
-  // 16w + 4rb .. +3.  Loads are clamped into range; rows past the slice are zeroed when stored,
-  // features past M / N hold finite in-range data whose outputs are never stored.
-  const int ca = lane & 31, ra = lane >> 5, cb = lane & 15, rb = lane >> 4;
-  const bool stage_b = w < 4;
-  // element offsets from the (wave-uniform) matrix bases fit 32 bits (B <= 2^20 rows of <= 512
-  // floats): scalar base + one 32-bit VGPR offset per load instead of a 64-bit lane address
-  const uint32_t a_col = (uint32_t)min(i0 + 4 * ca, M - 4);
-  const uint32_t b_col = (uint32_t)min(j0 + 4 * cb, N - 4);
-  // two register sets: the loads of chunk c + 2 are in flight while chunk c computes and chunk
-  // c + 1 (loaded during chunk c - 1) is staged
-  f32x4 pa0[4], pb0[4], pa1[4], pb1[4];
-  auto fetch = [&](int k0, f32x4(&pa)[4], f32x4(&pb)[4]) {
-    if (HWY_WG_EXP == 2 && k0 != kb0) return;
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const uint32_t k = (uint32_t)min(k0 + 8 * w + 4 * ra + jj, kb1 - 1);
-      pa[jj] = *reinterpret_cast<const f32x4*>(A + (k * (uint32_t)lda + a_col));
-    }
-    if (stage_b) {
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const uint32_t k = (uint32_t)min(k0 + 16 * w + 4 * rb + jj, kb1 - 1);
-        pb[jj] = *reinterpret_cast<const f32x4*>(Bm + (k * (uint32_t)ldb + b_col));
-      }
-    }
-  };
-  // column sums of A for the bias (kept for every tile, used when tj == 0)
-  float bsum[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  // staging pieces: 0-1 A columns 2p, 2p+1; 2-3 B columns 2p, 2p+1 (waves 0-3).  The
-  // transposing selects write straight into the ds_write_b128 data registers.
-  auto piece = [&](float* As, float* Bs, int k0, int pc, const f32x4(&pa)[4],
-                   const f32x4(&pb)[4]) {
-    if (pc < 2) {
-      const int kr = k0 + 8 * w + 4 * ra, q = 2 * w + ra;
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii) {
-        const int i = 2 * pc + ii;
-        f32x4 col;
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) col[jj] = kr + jj < kb1 ? pa[jj][i] : 0.0f;
-        *reinterpret_cast<f32x4*>(&As[wg_at(4 * ca + i, q)]) = col;
-        bsum[i] += ((col[0] + col[1]) + col[2]) + col[3];
-      }
-    } else if (stage_b) {
-      const int kr = k0 + 16 * w + 4 * rb, q = 4 * w + rb;
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii) {
-        const int i = 2 * (pc - 2) + ii;
-        f32x4 col;
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) col[jj] = kr + jj < kb1 ? pb[jj][i] : 0.0f;
-        *reinterpret_cast<f32x4*>(&Bs[wg_at(4 * cb + i, q)]) = col;
-      }
-    }
-  };
-  // MFMA: waves w and w + 4 (the two waves of one SIMD) own the same 64 x 32 output block
-  // (two 32x32 accumulators sharing the B operand) over the even / odd 8-row groups of every
-  // chunk: four independent accumulation chains per SIMD.
-  const int kh = w >> 2, wq = w & 3;
-  const int wm = (wq & 1) * 64, wn = (wq >> 1) * 32;
-  f32x16 acc0, acc1;
-#pragma unroll
-  for (int q = 0; q < 16; ++q) acc0[q] = acc1[q] = 0.0f;
-  auto chunk = [&](const float* As, const float* Bs, float* nA, float* nB, int k_next,
-                   const f32x4(&pa)[4], const f32x4(&pb)[4], auto stash_tag) {
-    constexpr bool STASH = decltype(stash_tag)::value;
-    f32x4 x0[2], x1[2], y[2];
-    auto rd = [&](int g, int b) {  // this wave's group g = row group 2g + kh of the chunk
-      const int q = 2 * (2 * g + kh) + h;
-      x0[b] = *reinterpret_cast<const f32x4*>(&As[wg_at(wm + l32, q)]);
-      x1[b] = *reinterpret_cast<const f32x4*>(&As[wg_at(wm + 32 + l32, q)]);
-      y[b] = *reinterpret_cast<const f32x4*>(&Bs[wg_at(wn + l32, q)]);
-    };
-    rd(0, 0);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int b = g & 1;
-      if (g + 1 < 4) rd(g + 1, b ^ 1);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (HWY_WG_EXP == 4) {
-          acc0[j] += x0[b][j] * y[b][j];
-          acc1[j] += x1[b][j] * y[b][j];
-          continue;
-        }
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(x0[b][j], y[b][j], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(x1[b][j], y[b][j], acc1, 0, 0, 0);
-      }
-      if constexpr (STASH && HWY_WG_EXP != 1) {
-        piece(nA, nB, k_next, g, pa, pb);
-        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);  // the next group's operand reads
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU (selects, bias adds)
-          if (u == 3 || u == 6) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // ds_write
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  float* buf0 = wg_lds;
-  float* buf1 = wg_lds + (kWgTM + kWgTN) * 64;
-  // loads past the slice are clamped (harmless, never stored)
-  fetch(kb0, pa0, pb0);
-  fetch(kb0 + 64, pa1, pb1);
-#pragma unroll
-  for (int pc = 0; pc < 4; ++pc) piece(buf0, buf0 + kWgTM * 64, kb0, pc, pa0, pb0);
-  fetch(kb0 + 128, pa0, pb0);
-  __syncthreads();
-  const std::integral_constant<bool, true> with_stash;
-  const std::integral_constant<bool, false> no_stash;
-  for (int c = 0; c < nchunk; c += 2) {
-    // even chunk c from buf0, chunk c + 1 (set 1) -> buf1, set 1 <- chunk c + 3
-    if (c + 1 < nchunk) {
-      chunk(buf0, buf0 + kWgTM * 64, buf1, buf1 + kWgTM * 64, kb0 + 64 * (c + 1), pa1, pb1,
-            with_stash);
-      if (c + 3 < nchunk) fetch(kb0 + 64 * (c + 3), pa1, pb1);
-    } else {
-      chunk(buf0, buf0 + kWgTM * 64, buf1, buf1 + kWgTM * 64, 0, pa1, pb1, no_stash);
-    }
-    if (HWY_WG_EXP != 3) __syncthreads();
-    if (c + 1 >= nchunk) break;
-    // odd chunk c + 1 from buf1, chunk c + 2 (set 0) -> buf0, set 0 <- chunk c + 4
-    if (c + 2 < nchunk) {
-      chunk(buf1, buf1 + kWgTM * 64, buf0, buf0 + kWgTM * 64, kb0 + 64 * (c + 2), pa0, pb0,
-            with_stash);
-      if (c + 4 < nchunk) fetch(kb0 + 64 * (c + 4), pa0, pb0);
-    } else {
-      chunk(buf1, buf1 + kWgTM * 64, buf0, buf0 + kWgTM * 64, 0, pa0, pb0, no_stash);
-    }
-    if (HWY_WG_EXP != 3) __syncthreads();
-  }
-  PSEC(8);
-  // waves 4-7 hand their accumulators to waves 0-3 through LDS (fixed order: even + odd groups)
-  float* xch = wg_lds;  // [4 waves][32 floats][64 lanes]
-  if (kh == 1) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      xch[(wq * 32 + q) * 64 + lane] = acc0[q];
-      xch[(wq * 32 + 16 + q) * 64 + lane] = acc1[q];
-    }
-  }
-  // bias partials of the 8 (w, ra) row sets per feature
-  float* bpart = wg_lds + 4 * 32 * 64;  // [16][128]
-#pragma unroll
-  for (int i = 0; i < 4; ++i) bpart[(2 * w + ra) * kWgTM + 4 * ca + i] = bsum[i];
-  __syncthreads();
-  if (kh == 0) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int ri = wm + (q & 3) + 8 * (q >> 2) + 4 * h;
-      WG_ST(&part[ri * kWgTN + wn + l32], acc0[q] + xch[(wq * 32 + q) * 64 + lane]);
-      WG_ST(&part[(ri + 32) * kWgTN + wn + l32], acc1[q] + xch[(wq * 32 + 16 + q) * 64 + lane]);
-    }
-  } else if (tj == 0 && t - 256 < kWgTM) {
-    const int f = t - 256;
-    float v = 0.0f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) v += bpart[r * kWgTM + f];
-    WG_ST(&part[kWgTM * kWgTN + f], v);
-  }
-  PSEC(9);
-}
-
-#if HWY_WG_DMA
 #define WGRAD_TILE wgrad_tile_dma
-#else
-#define WGRAD_TILE wgrad_tile
-#endif
 
 // Workgroups.  Default: tile * split + z -> tile `tile`, row slice z (rows [z ceil(B / split),
 // ...)), then the head-sum workgroups.  Slice z goes to workgroups with id % 8 = z, i.e. to one
@@ -2301,7 +2017,7 @@ __device__ __forceinline__ void ppo_wgrad_body(const WgArgs& a) {
   // one LDS array (a second __shared__ object beside the LDS-DMA images can make the compiler
   // drain every DMA before the first operand read of a chunk): the chunk buffers, then the
   // reduction slots
-  constexpr int kWgBufs = HWY_WG_DMA ? 3 : 2;
+  constexpr int kWgBufs = 3;
   __shared__ __attribute__((aligned(16))) float wg_lds[kWgBufs * (kWgTM + kWgTN) * 64 + kWgWaves + 2];
   float* red = wg_lds + kWgBufs * (kWgTM + kWgTN) * 64;
   const int ntile = a.tac + a.t2 + a.t1;
@@ -2354,17 +2070,9 @@ __global__ void __launch_bounds__(512) ppo_wgrad(WgArgs a) {
 
 // One ppo_wsum work item (1024 elements of a weight-gradient tile, 16 tile rows): the split
 // partial tiles summed in split order (deterministic) into the flat gradient, with all splits'
-// float4s in flight per thread, the bias sums of the tile's rows (work item 0 of the tile's
-// first column), and this thread's sum of squares.  gi / bi: the flat indices written (-1: none).
-struct WsumItem {
-  f32x4 v;
-  int64_t gi[4];
-  float b;
-  int64_t bi;
-  float sq;
-};
-
-__device__ __forceinline__ void wsum_item(const WgArgs& a, int item, WsumItem& it) {
+// float4s in flight per thread, and the bias sums of the tile's rows (work item 0 of the tile's
+// first column).  Returns this thread's sum of squares of what it wrote.
+__device__ __forceinline__ float wsum_item(const WgArgs& a, int item) {
   const int t = threadIdx.x, H = a.H;
   constexpr int kParts = kWgTM * kWgTN / 1024;
   const int tile_id = item / kParts, part = item % kParts;
@@ -2403,9 +2111,6 @@ __device__ __forceinline__ void wsum_item(const WgArgs& a, int item, WsumItem& i
   for (int q = 1; q < kMaxParts; ++q)
     if (q < np) v += pv[q];
   float sq = 0.0f;
-  it.v = v;
-#pragma unroll
-  for (int c4 = 0; c4 < 4; ++c4) it.gi[c4] = -1;
   if (i0 + ri < M) {
     const long row = grad_row(i0 + ri) + j0 + cj;
     float* dst = a.grads + row;
@@ -2414,11 +2119,8 @@ __device__ __forceinline__ void wsum_item(const WgArgs& a, int item, WsumItem& i
       if (j0 + cj + c4 < N) {
         dst[c4] = v[c4];
         sq += v[c4] * v[c4];
-        it.gi[c4] = row + c4;
       }
   }
-  it.b = 0.0f;
-  it.bi = -1;
   if (bias_t) {  // bias of output row i0 + t
     float b = 0.0f;
 #pragma unroll
@@ -2431,18 +2133,14 @@ __device__ __forceinline__ void wsum_item(const WgArgs& a, int item, WsumItem& i
     else bo = a.off[P_B1] + i;
     a.grads[bo] = b;
     sq += b * b;
-    it.b = b;
-    it.bi = bo;
   }
-  it.sq = sq;
+  return sq;
 }
 
 // ppo_wsum: every work item of every weight-gradient tile, one sum-of-squares partial each
 __global__ void __launch_bounds__(256) ppo_wsum(WgArgs a) {
   __shared__ float red[4];
-  WsumItem it;
-  wsum_item(a, blockIdx.x, it);
-  const float tot = block_sum4(it.sq, red);
+  const float tot = block_sum4(wsum_item(a, blockIdx.x), red);
   if (threadIdx.x == 0) a.norm_part[a.nh + blockIdx.x] = tot;
 }
 
@@ -2620,10 +2318,7 @@ __global__ void __launch_bounds__(kRedThreads) ppo_sumsq(const float* g, int64_t
   }
 }
 
-#ifndef HWY_ADAM_EPT
-#define HWY_ADAM_EPT 2
-#endif
-constexpr int kAdamEPT = HWY_ADAM_EPT;  // elements per thread (same box: 1 5.9 µs, 2 5.5, 4 5.7, 8 7.4)
+constexpr int kAdamEPT = 2;  // elements per thread (same box: 1 5.9 µs, 2 5.5, 4 5.7, 8 7.4)
 
 // clip_grad_norm_'s coefficient from the norm partials and Adam's bias corrections, into
 // sh[0] (coef), sh[1] (lr / bc1), sh[2] (sqrt bc2); every thread of the workgroup calls it
@@ -2745,7 +2440,9 @@ int64_t hwy_ppo_tile_image_offset(const hwy_ppo_dims* d) {
   return (int64_t)(reinterpret_cast<char*>(w.wtile) - base);
 }
 
-int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
+// ev (fused path only; measurement): events recorded before ppo_rows and after ppo_rows,
+// ppo_wgrad and ppo_wsum (hwy_ppo_time_kernels)
+static int forward_backward_ev(const hwy_ppo_args* a, void* stream, hipEvent_t* ev) {
   if (!a) return -1;
   const hwy_ppo_dims& d = a->dims;
   if (hwy_ppo_workspace_bytes(&d) < 0) return -1;
@@ -2768,6 +2465,7 @@ int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
     r.counters = a->counters;
     // 8 waves (2 per SIMD) when the columns split into 16-wide tiles, else 4
     const dim3 g1(w.n1), b4(256), b8(512), blk(256);
+    if (ev) rc |= hipEventRecord(ev[0], s) == hipSuccess ? 0 : -1;
     if (w.rt == 4 * kRowTile) {
       hipLaunchKernelGGL((ppo_rows_c64<4, 8>), g1, b8, 0, s, r);
     } else if (w.rt == 2 * kRowTile) {
@@ -2776,10 +2474,7 @@ int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
         case 2: hipLaunchKernelGGL((ppo_rows<2, 8, 32>), g1, b8, 0, s, r); break;
         case 3: hipLaunchKernelGGL((ppo_rows<3, 4, 32>), g1, b4, 0, s, r); break;
         default:
-          if (HWY_ROWS_CMP && HWY_ROWS_NW32 == 8)
-            hipLaunchKernelGGL((ppo_rows_c<4, 8, 32>), g1, b8, 0, s, r);
-          else
-            hipLaunchKernelGGL((ppo_rows<4, HWY_ROWS_NW32, 32>), g1, dim3(64 * HWY_ROWS_NW32), 0, s, r);
+          hipLaunchKernelGGL((ppo_rows_c<4, 8, 32>), g1, b8, 0, s, r);
           break;
       }
     } else {
@@ -2787,7 +2482,7 @@ int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
         case 1: hipLaunchKernelGGL((ppo_rows<1, 4, 16>), g1, b4, 0, s, r); break;
         case 2: hipLaunchKernelGGL((ppo_rows<2, 8, 16>), g1, b8, 0, s, r); break;
         case 3: hipLaunchKernelGGL((ppo_rows<3, 4, 16>), g1, b4, 0, s, r); break;
-        case 4: hipLaunchKernelGGL((ppo_rows<4, HWY_ROWS_NW, 16>), g1, dim3(64 * HWY_ROWS_NW), 0, s, r); break;
+        case 4: hipLaunchKernelGGL((ppo_rows<4, 8, 16>), g1, b8, 0, s, r); break;
         case 5: hipLaunchKernelGGL((ppo_rows<5, 4, 16>), g1, b4, 0, s, r); break;
         case 6: hipLaunchKernelGGL((ppo_rows<6, 8, 16>), g1, b8, 0, s, r); break;
         case 7: hipLaunchKernelGGL((ppo_rows<7, 4, 16>), g1, b4, 0, s, r); break;
@@ -2795,6 +2490,7 @@ int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
       }
     }
     rc |= hipGetLastError() == hipSuccess ? 0 : -1;
+    if (ev) rc |= hipEventRecord(ev[1], s) == hipSuccess ? 0 : -1;
     WgArgs g = {};
     g.B = B, g.S = S, g.H = H;
     g.dac = w.dac, g.h2 = w.h2, g.dh2 = w.dh2, g.h1 = w.h1, g.dh1 = w.dh1, g.xg = w.xg;
@@ -2809,10 +2505,13 @@ int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
     g.params = P, g.metrics = a->metrics, g.counters = a->counters;
     hipLaunchKernelGGL(ppo_wgrad, dim3(w.grid2), dim3(64 * kWgWaves), 0, s, g);
     rc |= hipGetLastError() == hipSuccess ? 0 : -1;
+    if (ev) rc |= hipEventRecord(ev[2], s) == hipSuccess ? 0 : -1;
     hipLaunchKernelGGL(ppo_wsum, dim3((w.tac + w.t2 + w.t1) * (kWgTM * kWgTN / 1024)), blk, 0, s, g);
     rc |= hipGetLastError() == hipSuccess ? 0 : -1;
+    if (ev) rc |= hipEventRecord(ev[3], s) == hipSuccess ? 0 : -1;
     return rc;
   }
+  if (ev) return -1;  // the per-kernel timing covers the fused path only
   // ---- forward (general path: separate GEMMs, split-K weight gradients)
   {
     GemmArgs g = gemm_args();
@@ -2928,6 +2627,10 @@ int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
   return rc;
 }
 
+int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
+  return forward_backward_ev(a, stream, nullptr);
+}
+
 int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream) {
   if (!a) return -1;
   const hwy_ppo_dims& d = a->dims;
@@ -2955,6 +2658,38 @@ int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream) {
   const int nadam = (int)((L.numel + 256 * kAdamEPT - 1) / (256 * kAdamEPT));
   hipLaunchKernelGGL(ppo_adam, dim3(nadam), dim3(256), 0, s, o);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int hwy_ppo_time_kernels(const hwy_ppo_args* a, void* stream, int reps, float* us) {
+  if (!a || !us || reps < 1 || a->grads_modified) return -1;
+  if (hwy_ppo_workspace_bytes(&a->dims) < 0 || !fused_ok(a->dims)) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  hipEvent_t ev[5];
+  int made = 0, rc = 0;
+  for (; made < 5; ++made)
+    if (hipEventCreate(&ev[made]) != hipSuccess) {
+      rc = -2;
+      break;
+    }
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int i = 0; i < reps && rc == 0; ++i) {
+    rc |= forward_backward_ev(a, stream, ev);
+    rc |= hwy_ppo_optimizer(a, stream);
+    rc |= hipEventRecord(ev[4], s) == hipSuccess ? 0 : -1;
+    if (rc || hipEventSynchronize(ev[4]) != hipSuccess) {
+      rc = rc ? rc : -2;
+      break;
+    }
+    for (int k = 0; k < 4; ++k) {
+      float ms = 0.0f;
+      if (hipEventElapsedTime(&ms, ev[k], ev[k + 1]) != hipSuccess) rc = -2;
+      acc[k] += ms;
+    }
+  }
+  for (int k = 0; k < made; ++k) (void)hipEventDestroy(ev[k]);
+  if (rc) return rc;
+  for (int k = 0; k < 4; ++k) us[k] = (float)(acc[k] * 1e3 / reps);
+  return 0;
 }
 
 int hwy_ppo_sync_params(const hwy_ppo_args* a, void* stream) {
@@ -2994,7 +2729,7 @@ int hwy_ppo_act(const hwy_ppo_act_args* a, void* stream) {
       case 1: hipLaunchKernelGGL((ppo_act<1, 4, TL>), g, b4, 0, s, r); break;
       case 2: hipLaunchKernelGGL((ppo_act<2, 8, TL>), g, b8, 0, s, r); break;
       case 3: hipLaunchKernelGGL((ppo_act<3, 4, TL>), g, b4, 0, s, r); break;
-      case 4: hipLaunchKernelGGL((ppo_act<4, HWY_ACT_NW, TL>), g, dim3(64 * HWY_ACT_NW), 0, s, r); break;
+      case 4: hipLaunchKernelGGL((ppo_act<4, 8, TL>), g, b8, 0, s, r); break;
       case 5: hipLaunchKernelGGL((ppo_act<5, 4, TL>), g, b4, 0, s, r); break;
       case 6: hipLaunchKernelGGL((ppo_act<6, 8, TL>), g, b8, 0, s, r); break;
       case 7: hipLaunchKernelGGL((ppo_act<7, 4, TL>), g, b4, 0, s, r); break;
@@ -3003,7 +2738,7 @@ int hwy_ppo_act(const hwy_ppo_act_args* a, void* stream) {
   };
   // H = 256 from the tile image: the compact kernel, 32-row tiles once there are two per CU
   // (16,384 rows on MI355X: 91.3 -> 69.4 us), else 16-row tiles (4,096 rows: 25.1 -> 22.0 us)
-  if (HWY_ACT_CMP && r.tiles && d.H == 256) {
+  if (r.tiles && d.H == 256) {
     if (d.B >= 64 * chip_geom().cus)
       hipLaunchKernelGGL((ppo_act_c<4, 8, 32>), dim3((d.B + 31) / 32), b8, 0, s, r);
     else

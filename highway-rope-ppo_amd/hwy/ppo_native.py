@@ -70,6 +70,9 @@ def _bind(L):
     L.hwy_ppo_sync_params.restype = ctypes.c_int
     L.hwy_ppo_act.argtypes = [ctypes.POINTER(PpoActArgs), ctypes.c_void_p]
     L.hwy_ppo_act.restype = ctypes.c_int
+    L.hwy_ppo_time_kernels.argtypes = [ctypes.POINTER(PpoArgs), ctypes.c_void_p, ctypes.c_int,
+                                       ctypes.c_void_p]
+    L.hwy_ppo_time_kernels.restype = ctypes.c_int
     L.hwy_ppo_tile_image_offset.argtypes = [ctypes.POINTER(PpoDims)]
     L.hwy_ppo_tile_image_offset.restype = ctypes.c_int64
     L._ppo_bound = True
@@ -120,6 +123,15 @@ def flat_params(agent):
     return agent._flat
 
 
+def _param_versions(agent, flat: torch.Tensor, params) -> tuple:
+    """What a weight tile image is in step with: in-place writes through a parameter
+    (load_state_dict, an eager torch optimizer step) bump that parameter's version counter, writes
+    through the flat buffer bump the buffer's, and a graph-replayed torch learner, which writes in
+    place without bumping either, counts in agent._torch_param_writes."""
+    return ((getattr(agent, "_torch_param_writes", 0), flat._version)
+            + tuple(p._version for p in params))
+
+
 # hidden width at which hwy_ppo_act runs ppo_act_c, the forward + head of the minibatch step's
 # compact row kernel, from a weight tile image (ppo_kernels.hip: hwy_ppo_act)
 _ACT_C_HIDDEN = 256
@@ -134,6 +146,7 @@ class _TileImage:
     def __init__(self, agent, flat: torch.Tensor, S: int, H: int):
         L = _bind(lib())
         self.L, self.flat, self.S = L, flat, S
+        self.agent = agent
         self.params = flat_params(agent)[3]
         self.dims = PpoDims(64, S, H, 2)
         ws = L.hwy_ppo_workspace_bytes(ctypes.byref(self.dims))
@@ -145,7 +158,7 @@ class _TileImage:
         self.version = None
 
     def _versions(self):
-        return (self.flat._version,) + tuple(p._version for p in self.params)
+        return _param_versions(self.agent, self.flat, self.params)
 
     def current(self) -> int:
         if self.version != self._versions():
@@ -360,9 +373,7 @@ class FusedPPO:
         return self.workspace.data_ptr() + self._tile_off
 
     def _param_versions(self):
-        # in-place writes through a parameter (load_state_dict, a torch optimizer step) bump that
-        # parameter's counter, writes through the flat buffer bump the buffer's
-        return (self.flat._version,) + tuple(p._version for p in self.params)
+        return _param_versions(self.agent, self.flat, self.params)
 
     def _allreduce(self):
         if self._avg_op:  # RCCL averages in the collective (no extra division kernel)
@@ -392,6 +403,7 @@ class FusedPPO:
                ret.data_ptr(), perm.data_ptr()) + self._scalar_key()
         args = [self._args(states, pre_tanh, old_lp, adv, ret, perm.data_ptr() + i * mb * 8)
                 for i in range(nmb)]
+        self._last_args = args
         self.counters[1].zero_()
         # the weight tile image the row kernel streams: params may have been written since the
         # last update (checkpoint load, torch optimizer); hwy_ppo_optimizer keeps it in step
@@ -420,6 +432,28 @@ class FusedPPO:
             self._epoch_event(ev)
         self._tiles_version = self._param_versions()
         return self.metrics
+
+    KERNELS = ("ppo_rows", "ppo_wgrad", "ppo_wsum", "ppo_adam")
+
+    def time_kernels(self, reps: int = 16) -> Optional[dict]:
+        """Average microseconds per launch of each kernel of the minibatch step (ppo_rows,
+        ppo_wgrad, ppo_wsum, ppo_adam), event to event over `reps` eager steps on the last
+        update's first minibatch (hwy_ppo_time_kernels).  A measurement aid for bench.py, run
+        after its timed region: the steps update the weights and Adam state as training steps
+        do, and metrics rows 0 .. reps - 1 are overwritten.  None before the first run()."""
+        args = getattr(self, "_last_args", None)
+        if not args:
+            return None
+        reps = max(1, min(int(reps), self.metrics.shape[0]))
+        a = PpoArgs.from_buffer_copy(args[0])
+        a.grads_modified = 0  # this rank's own kernels only (no all-reduce between them)
+        self.counters[1].zero_()
+        us = (ctypes.c_float * 4)()
+        check(self.L.hwy_ppo_time_kernels(ctypes.byref(a), stream_ptr(), reps, us),
+              "hwy_ppo_time_kernels")
+        self.counters[1].zero_()
+        self._tiles_version = self._param_versions()
+        return dict(zip(self.KERNELS, (float(u) for u in us)))
 
     def _epoch_event(self, start=None):
         if self.epoch_events is None:

@@ -405,6 +405,10 @@ class PPOAgent:
         self._adam_owner = "torch"
         self._warned_ragged = False
         self.updates = 0  # completed update() / update_rollout() calls (evaluation memo key)
+        # torch-path optimizer runs: a graph-replayed torch learner writes the parameters in
+        # place without bumping their version counters, so the fused path's weight tile images
+        # key their staleness on this count too (hwy/ppo_native.py)
+        self._torch_param_writes = 0
         self.generator = None
         if self.device.type == "cuda":
             self.generator = torch.Generator(device=self.device)
@@ -496,6 +500,7 @@ class PPOAgent:
 
     def _run_epochs(self, states, pre_tanh, old_logp, adv, ret, batches: List[torch.Tensor]):
         self._adam_to("torch")
+        self._torch_param_writes += 1  # retires every fused tile image (see __init__)
         n = states.shape[0]
         sizes = {int(b.numel()) for b in batches}
         mb = max(sizes)

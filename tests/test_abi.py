@@ -117,6 +117,30 @@ def test_product_library_holds_only_reachable_row_kernels():
     transposed ppo_rowsT row kernel was compiled in but reachable only through a dev knob)."""
     blob = open(LIB_PATH, "rb").read()
     assert b"ppo_rowsT" not in blob
-    for name in (b"ppo_rows_c", b"ppo_wgrad", b"ppo_wsum", b"ppo_adam", b"ppo_act_c",
-                 b"hwy_step_kernel"):
+    # mangled names (length-prefixed), so that ppo_rows_c64 does not also satisfy ppo_rows_c
+    # (ADVICE r4): the 32-row compact tile and the 64-row tile are separate kernels
+    for name in (b"10ppo_rows_cILi4ELi8ELi32E", b"12ppo_rows_c64ILi4ELi8E", b"ppo_wgrad",
+                 b"ppo_wsum", b"ppo_adam", b"ppo_act_c", b"hwy_step_kernel"):
         assert name in blob, name
+    # H = 256's 32-row tiles always run the compact kernel: the plain one is not built
+    assert b"8ppo_rowsILi4ELi8ELi32E" not in blob
+
+
+def test_kernel_sources_carry_no_ab_knob_forest():
+    """the measured-and-rejected A/B alternatives are gone from the product
+    kernel sources; what remains for development sits behind HWY_DEV_KNOBS (the partition knobs
+    of ppo_kernels.hip's dev block, the timing-only pricing masks of hwy_dev_knobs.h)."""
+    import glob
+    import re
+
+    csrc = os.path.join(ROOT, "highway-rope-ppo_amd", "csrc")
+    n = 0
+    for path in glob.glob(os.path.join(csrc, "*.hip")):
+        src = open(path).read()
+        n += len(re.findall(r"^#ifndef HWY_", src, flags=re.M))
+        # timing-only (wrong-result) builds are reachable only through the dev header
+        assert "HWY_SKIP" not in src, path
+        assert "HWY_WG_EXP" not in src and "HWY_WG_TEAMS" not in src, path
+    assert n <= 3
+    dev = open(os.path.join(csrc, "hwy_dev_knobs.h")).read()
+    assert "HWY_SKIP" in dev

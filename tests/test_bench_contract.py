@@ -36,7 +36,8 @@ def test_cli_defaults(monkeypatch):
     a = b.parse()
     assert (a.gpus, a.steps, a.warmup, a.config, a.hidden, a.epochs, a.minibatches) == \
         (1, 20, 5, 1, 256, 8, 32)
-    assert b.CONFIGS[1] == dict(envs=4096, obs=15, order="sorted", pe="none", d=0, rollout=128)
+    # the reward-faithful recipe is the default line: 4,096-row minibatches
+    assert b.CONFIGS[1] == dict(envs=4096, obs=15, order="sorted", pe="none", d=0, rollout=32)
 
 
 def test_config_table_matches_baseline_json():

@@ -45,3 +45,18 @@ def test_bench_two_ranks_one_line():
     assert ar["bytes"] == 4 * n_params and ar["us_per_allreduce"] > 0
     assert roof["step_us_with_allreduce"] == roof["avg_launch_us"] > 0
     assert 0 < roof["allreduce_share_of_step"] == round(ar["us_per_allreduce"] / roof["avg_launch_us"], 4)
+    # the line proves its ranks from the communicator: world size and backend
+    # as the process group reports them, every rank's device and PCI location, whether the epoch
+    # graph captured the collective; gloo rehearses both ranks on one GPU (one distinct device)
+    rk = d["config"]["ranks"]
+    assert rk["world_size"] == 2 and rk["backend"] == "gloo"
+    assert sorted(r["rank"] for r in rk["per_rank"]) == [0, 1]
+    assert all(r["pci"] and r["device"] == 0 for r in rk["per_rank"])
+    assert rk["distinct_devices"] == 1
+    assert d["config"]["epoch_graph_collectives"] in ("captured",
+                                                      "per-step graphs, all-reduce between them")
+    # per-kernel times of the step beside the epoch-event step time
+    pk = roof["per_kernel"]
+    assert set(pk) >= {"ppo_rows", "ppo_wgrad", "ppo_wsum", "ppo_adam", "sum_us", "method"}
+    assert all(pk[k]["us"] > 0 for k in ("ppo_rows", "ppo_wgrad", "ppo_wsum", "ppo_adam"))
+    assert roof["flops_required_per_launch"] < roof["flops_per_launch"]

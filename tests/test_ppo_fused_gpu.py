@@ -636,3 +636,36 @@ def test_adam_state_hands_over_between_fused_and_eager_updates():
     for (k, va), (_, vb) in zip(a.actor_critic.state_dict().items(), b.actor_critic.state_dict().items()):
         d = (va - vb).abs()
         assert (d > 2e-5).float().mean().item() < 0.05, (k, d.max().item())
+
+
+def test_act_after_graph_replayed_reference_updates():
+    """the reference path's update() replays a captured torch learner, which writes the
+    parameters in place without bumping their version counters.  Batched acting at H = 256 runs
+    ppo_act_c from a cached weight tile image, so that image must be retired by every such update
+    (agent._torch_param_writes) or acting would use the previous update's weights."""
+    from hwy.ppo_native import fused_act
+    from ppo.agent import PPOAgent
+
+    S, H = 60, 256
+    torch.manual_seed(3)
+    ag = PPOAgent(S, 2, lr=1e-3, epochs=2, batch_size=64, hidden_dim=H, device=DEV,
+                  use_graphs=True, backend="hip")
+    x = torch.randn(512, S, device=DEV)
+    with torch.no_grad():
+        fused_act(ag, x, deterministic=True)  # builds the acting-only tile image
+    rng = np.random.default_rng(0)
+    for _ in range(3):
+        before = [p.detach().clone() for p in ag.actor_critic.parameters()]
+        for i in range(256):
+            s = rng.standard_normal(S).astype(np.float32)
+            a, z, lp, v = ag.select_action(s)
+            ag.memory.store(s, a, z, float(rng.standard_normal()), s, lp, i % 50 == 49, v)
+        ag.update(0.0)
+        moved = max(float((p.detach() - b).abs().max())
+                    for p, b in zip(ag.actor_critic.parameters(), before))
+        assert moved > 1e-4  # the update wrote the weights
+        with torch.no_grad():
+            ref = ag.actor_critic.act(x, deterministic=True)
+            got = fused_act(ag, x, deterministic=True)
+        for r, g in zip(ref, got):
+            torch.testing.assert_close(g, r, rtol=1e-4, atol=2e-5)
