@@ -114,6 +114,9 @@ constexpr int kMaxRowS = 256;  // states dim bound of the fused path (LDS)
 //    groups of the current one;
 //  - kRingDC weight blocks in flight per wave in the compact-LDS row kernels.
 constexpr int kRingDC = 2;
+#ifndef HWY_ROWS_XCD
+#define HWY_ROWS_XCD 0  // A/B (round 5): row tiles clustered by XCD for ppo_wgrad's slices
+#endif
 constexpr int kWgTM = 128, kWgTN = 64;          // ppo_wgrad output tile
 constexpr int kWgWaves = 8;                     // ppo_wgrad waves (2 per SIMD)
 constexpr int kWgPart = kWgTM * kWgTN + kWgTM;  // floats per partial tile (+ bias sums)
@@ -810,11 +813,19 @@ struct RowArgs {
   float *h1, *h2, *dac, *dh2, *dh1;
   float* xg;         // [B][S] gathered states (ppo_wgrad's dW1 operand)
   const float* tiles;  // weight tile image (TileGeom), in sync with params
-  float* head_part;  // [gridDim.x][HP]
+  float* head_part;  // [gridDim.x][HP], one row per row tile
   int HP;
   float eps_clip, value_coef, entropy_coef;
   int32_t* counters;
+  int xgrp;  // > 1: row tiles clustered by workgroup id mod xgrp (row_tile_of)
 };
+
+// The row tile of workgroup b of n.  xgrp > 1 (and n % xgrp == 0): workgroups b = xgrp k + z take
+// tiles z n / xgrp + k, so under round-robin placement the tiles of ppo_wgrad's row slice z are
+// produced on the XCD that reads them (speed only; the results do not depend on placement).
+__device__ __forceinline__ int row_tile_of(int b, int n, int xgrp) {
+  return (xgrp > 1 && n % xgrp == 0) ? (b % xgrp) * (n / xgrp) + b / xgrp : b;
+}
 
 // Row pitch (floats) of the row kernels' LDS images for n columns (n % 16 == 0): n + 8, i.e. a
 // quad pitch = 2 mod 4.  The MFMA operand reads (ds_read_b128, lane (g, c) reads quad
@@ -1284,7 +1295,8 @@ __device__ __forceinline__ void rows_body(const RowArgs& r) {
   PSEC_DECL
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int S = r.S;
-  const int row0 = blockIdx.x * RT;
+  const int tile = row_tile_of(blockIdx.x, gridDim.x, r.xgrp);
+  const int row0 = tile * RT;
   const int nrows = min(RT, r.B - row0);
   const float* P = r.params;
   constexpr int D = CMP ? kRingDC : ring_depth<TW>();  // CMP: 4 waves per SIMD hide more
@@ -1429,7 +1441,7 @@ __device__ __forceinline__ void rows_body(const RowArgs& r) {
           gc[u] += dv * cc;
         }
       }
-    float* out = r.head_part + (long)blockIdx.x * r.HP;
+    float* out = r.head_part + (long)tile * r.HP;
 #pragma unroll
     for (int u = 0; u < TW; ++u) {
       // lanes c, c+16, c+32, c+48 hold the same column: (g0 + g1) + (g2 + g3)
@@ -2440,9 +2452,9 @@ int64_t hwy_ppo_tile_image_offset(const hwy_ppo_dims* d) {
   return (int64_t)(reinterpret_cast<char*>(w.wtile) - base);
 }
 
-// ev (fused path only; measurement): events recorded before ppo_rows and after ppo_rows,
-// ppo_wgrad and ppo_wsum (hwy_ppo_time_kernels)
-static int forward_backward_ev(const hwy_ppo_args* a, void* stream, hipEvent_t* ev) {
+// mask (fused path; hwy_ppo_time_kernels launches them one at a time): bit 0 ppo_rows, bit 1
+// ppo_wgrad, bit 2 ppo_wsum
+static int forward_backward_k(const hwy_ppo_args* a, void* stream, int mask) {
   if (!a) return -1;
   const hwy_ppo_dims& d = a->dims;
   if (hwy_ppo_workspace_bytes(&d) < 0) return -1;
@@ -2463,10 +2475,12 @@ static int forward_backward_ev(const hwy_ppo_args* a, void* stream, hipEvent_t* 
     r.head_part = w.head_part, r.HP = w.HP;
     r.eps_clip = a->eps_clip, r.value_coef = a->value_coef, r.entropy_coef = a->entropy_coef;
     r.counters = a->counters;
+    // wgrad's row slices one per XCD: the row tiles of slice z made on the XCD that reads them
+    r.xgrp = (HWY_ROWS_XCD && w.split == chip_geom().xcds) ? w.split : 0;
     // 8 waves (2 per SIMD) when the columns split into 16-wide tiles, else 4
     const dim3 g1(w.n1), b4(256), b8(512), blk(256);
-    if (ev) rc |= hipEventRecord(ev[0], s) == hipSuccess ? 0 : -1;
-    if (w.rt == 4 * kRowTile) {
+    if (!(mask & 1)) {
+    } else if (w.rt == 4 * kRowTile) {
       hipLaunchKernelGGL((ppo_rows_c64<4, 8>), g1, b8, 0, s, r);
     } else if (w.rt == 2 * kRowTile) {
       switch (H / 64) {
@@ -2490,7 +2504,6 @@ static int forward_backward_ev(const hwy_ppo_args* a, void* stream, hipEvent_t* 
       }
     }
     rc |= hipGetLastError() == hipSuccess ? 0 : -1;
-    if (ev) rc |= hipEventRecord(ev[1], s) == hipSuccess ? 0 : -1;
     WgArgs g = {};
     g.B = B, g.S = S, g.H = H;
     g.dac = w.dac, g.h2 = w.h2, g.dh2 = w.dh2, g.h1 = w.h1, g.dh1 = w.dh1, g.xg = w.xg;
@@ -2503,15 +2516,14 @@ static int forward_backward_ev(const hwy_ppo_args* a, void* stream, hipEvent_t* 
     g.entropy_coef = a->entropy_coef, g.value_coef = a->value_coef;
     g.ent_const = 0.5f + 0.91893853320467274178f;
     g.params = P, g.metrics = a->metrics, g.counters = a->counters;
-    hipLaunchKernelGGL(ppo_wgrad, dim3(w.grid2), dim3(64 * kWgWaves), 0, s, g);
+    if (mask & 2) hipLaunchKernelGGL(ppo_wgrad, dim3(w.grid2), dim3(64 * kWgWaves), 0, s, g);
     rc |= hipGetLastError() == hipSuccess ? 0 : -1;
-    if (ev) rc |= hipEventRecord(ev[2], s) == hipSuccess ? 0 : -1;
-    hipLaunchKernelGGL(ppo_wsum, dim3((w.tac + w.t2 + w.t1) * (kWgTM * kWgTN / 1024)), blk, 0, s, g);
+    if (mask & 4)
+      hipLaunchKernelGGL(ppo_wsum, dim3((w.tac + w.t2 + w.t1) * (kWgTM * kWgTN / 1024)), blk, 0, s, g);
     rc |= hipGetLastError() == hipSuccess ? 0 : -1;
-    if (ev) rc |= hipEventRecord(ev[3], s) == hipSuccess ? 0 : -1;
     return rc;
   }
-  if (ev) return -1;  // the per-kernel timing covers the fused path only
+  if (mask != 7) return -1;  // the per-kernel timing covers the fused path only
   // ---- forward (general path: separate GEMMs, split-K weight gradients)
   {
     GemmArgs g = gemm_args();
@@ -2628,7 +2640,7 @@ static int forward_backward_ev(const hwy_ppo_args* a, void* stream, hipEvent_t* 
 }
 
 int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream) {
-  return forward_backward_ev(a, stream, nullptr);
+  return forward_backward_k(a, stream, 7);
 }
 
 int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream) {
@@ -2661,35 +2673,62 @@ int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream) {
 }
 
 int hwy_ppo_time_kernels(const hwy_ppo_args* a, void* stream, int reps, float* us) {
-  if (!a || !us || reps < 1 || a->grads_modified) return -1;
+  if (!a || !us || reps < 1 || a->grads_modified || !a->counters) return -1;
   if (hwy_ppo_workspace_bytes(&a->dims) < 0 || !fused_ok(a->dims)) return -1;
-  hipStream_t s = (hipStream_t)stream;
-  hipEvent_t ev[5];
-  int made = 0, rc = 0;
-  for (; made < 5; ++made)
-    if (hipEventCreate(&ev[made]) != hipSuccess) {
+  // Each kernel as its own HIP graph of `reps` back-to-back launches on a private stream,
+  // replayed once to warm up and once between two events: the average launch of a kernel in the
+  // same position it has in the epoch graph (graph-issued, dependent on its predecessor), without
+  // host launch costs.  The caller's Adam step count is restored afterwards; the metrics row
+  // index is reset before each replay so ppo_wgrad always writes metrics row 0.
+  if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return -2;
+  int32_t saved[2];
+  if (hipMemcpy(saved, a->counters, sizeof(saved), hipMemcpyDeviceToHost) != hipSuccess) return -2;
+  hipStream_t s = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = 0;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)
+    rc = -2;
+  const int32_t one = 1;
+  for (int k = 0; k < 4 && rc == 0; ++k) {
+    hipGraph_t g = nullptr;
+    hipGraphExec_t x = nullptr;
+    if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) {
       rc = -2;
       break;
     }
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int i = 0; i < reps && rc == 0; ++i) {
-    rc |= forward_backward_ev(a, stream, ev);
-    rc |= hwy_ppo_optimizer(a, stream);
-    rc |= hipEventRecord(ev[4], s) == hipSuccess ? 0 : -1;
-    if (rc || hipEventSynchronize(ev[4]) != hipSuccess) {
-      rc = rc ? rc : -2;
-      break;
+    for (int i = 0; i < reps; ++i) {
+      if (k < 3)
+        rc |= forward_backward_k(a, s, 1 << k);
+      else
+        rc |= hwy_ppo_optimizer(a, s);
     }
-    for (int k = 0; k < 4; ++k) {
-      float ms = 0.0f;
-      if (hipEventElapsedTime(&ms, ev[k], ev[k + 1]) != hipSuccess) rc = -2;
-      acc[k] += ms;
+    rc |= hipStreamEndCapture(s, &g) == hipSuccess ? 0 : -2;
+    if (rc == 0) rc = hipGraphInstantiate(&x, g, nullptr, nullptr, 0) == hipSuccess ? 0 : -2;
+    for (int rep = 0; rep < 2 && rc == 0; ++rep) {
+      rc |= hipMemcpyAsync(a->counters + 1, &one, sizeof(one), hipMemcpyHostToDevice, s) ==
+                    hipSuccess ? 0 : -2;
+      if (rep) rc |= hipEventRecord(e0, s) == hipSuccess ? 0 : -2;
+      rc |= hipGraphLaunch(x, s) == hipSuccess ? 0 : -2;
+      if (rep) rc |= hipEventRecord(e1, s) == hipSuccess ? 0 : -2;
+      rc |= hipStreamSynchronize(s) == hipSuccess ? 0 : -2;
     }
+    float ms = 0.0f;
+    if (rc == 0) rc = hipEventElapsedTime(&ms, e0, e1) == hipSuccess ? 0 : -2;
+    us[k] = ms * 1e3f / (float)reps;
+    if (x) (void)hipGraphExecDestroy(x);
+    if (g) (void)hipGraphDestroy(g);
   }
-  for (int k = 0; k < made; ++k) (void)hipEventDestroy(ev[k]);
-  if (rc) return rc;
-  for (int k = 0; k < 4; ++k) us[k] = (float)(acc[k] * 1e3 / reps);
-  return 0;
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (s) {
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
+  }
+  saved[1] = 0;
+  if (hipMemcpy(a->counters, saved, sizeof(saved), hipMemcpyHostToDevice) != hipSuccess) rc = -2;
+  (void)hipGetLastError();
+  return rc;
 }
 
 int hwy_ppo_sync_params(const hwy_ppo_args* a, void* stream) {

@@ -72,12 +72,13 @@ typedef struct hwy_ppo_args {
 int hwy_ppo_forward_backward(const hwy_ppo_args* a, void* stream);
 /* clip_grad_norm_(max_grad_norm) + Adam step on params (call after any gradient all-reduce). */
 int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream);
-/* Measurement aid (bench.py's per-kernel roofline): `reps` minibatch steps -- the effects of
- * hwy_ppo_forward_backward + hwy_ppo_optimizer, Adam step included -- launched on `stream` with a
- * HIP event between consecutive kernels; waits for them and writes the average microseconds of
- * each launch (event to event) to us[4]: ppo_rows, ppo_wgrad, ppo_wsum, ppo_adam.  Fused path and
- * one process only (grads_modified == 0).  Synchronous, not graph-capturable; -1 bad args,
- * -2 HIP error. */
+/* Measurement aid (bench.py's per-kernel roofline): each kernel of the minibatch step
+ * (ppo_rows, ppo_wgrad, ppo_wsum, ppo_adam) captured as a HIP graph of `reps` back-to-back
+ * launches on a private stream and replayed between two events; writes the average microseconds
+ * per launch to us[4].  The Adam launches update params / moments / the tile image as training
+ * steps do; the Adam step count is restored and the metrics row index left at 0.  Waits for
+ * `stream` first; synchronous, not graph-capturable; fused path, grads_modified == 0.
+ * -1 bad args, -2 HIP error. */
 int hwy_ppo_time_kernels(const hwy_ppo_args* a, void* stream, int reps, float* us);
 /* Rebuild the workspace's weight tile image from params (uses dims, params, workspace). */
 int hwy_ppo_sync_params(const hwy_ppo_args* a, void* stream);
