@@ -229,7 +229,8 @@ __device__ __forceinline__ float idm_free(float ev_spd, float ev_tsp, float delt
   float tsp = hm_clipf(ev_tsp, 0.0f, limit);
   float base = hm_maxf(ev_spd, 0.0f) / hm_absf(hm_not_zero(tsp));
   if (kSkip & 32) return hm_fma(-COMFORT_ACC_MAX, base * base, COMFORT_ACC_MAX);
-  return hm_fma(-COMFORT_ACC_MAX, hm_powf(base, delta), COMFORT_ACC_MAX);
+  // np.power(base, DELTA): hm_powf's arithmetic, branch-free (bit-identical, hwy_math.h)
+  return hm_fma(-COMFORT_ACC_MAX, hm_powf_idm(base, delta), COMFORT_ACC_MAX);
 }
 
 // IDMVehicle.acceleration given its free-road term `acc` (interaction with the front vehicle)
@@ -1340,6 +1341,7 @@ __global__ void hwy_math_kernel(int op, const float* in, const float* in2, float
     case 12: { float c_; hm_sincosf(x, &r, &c_); } break;
     case 13: { float s_; hm_sincosf(x, &s_, &r); } break;
     case 14: r = hm_tanf_sc(x); break;
+    case 15: r = hm_powf_idm(x, y); break;
   }
   out[i] = r;
 }

@@ -298,6 +298,56 @@ HWY_HD float hm_powf(float b, float p) {
   return hm_expf(p * hm_logf(b));
 }
 
+/* np.power(b, p) for the IDM free-road term -- b = max(v, 0) / |target speed| (>= 0, or NaN),
+ * p = DELTA in [3.5, 4.5] -- as one short branch-free sequence (the general
+ * hm_powf costs ~100 VALU and 10 exec-mask branches per call on gfx950, once per vehicle and
+ * frame).  exp(p * log b) with Cephes' logf / expf polynomials, but: the mantissa taken in
+ * [sqrt(1/2), sqrt(2)) straight from the bits (no frexp, no subnormal path: a subnormal b gives
+ * a result below 2^-400, i.e. 0), 2^n built from its bits for n in [-126, 127], and the special
+ * cases as selects: b = 0 -> 0, NaN -> NaN, +inf -> +inf, exp overflow (p log b > 88) -> +inf,
+ * underflow (< -87) -> 0.  Inside that range every operation is hm_powf's, in its order, so the
+ * result is hm_powf's bit for bit for every normal b (tests/test_oracle_golden.py); the IDM's
+ * bases (<= 4,000) never reach the ends, where hm_powf would return a subnormal or a finite
+ * value above e^88 (3 (1 - b^p) rounds the same either way).  The same operations on the host and
+ * on gfx950 (correctly rounded primitives, explicit fma): the oracle and the kernel agree bit for
+ * bit. */
+HWY_HD float hm_powf_idm(float b, float p) {
+  const uint32_t u = hm_f2bits(b);
+  int e = (int)(u >> 23) - 127;
+  float m = hm_bits2f((u & 0x007fffffu) | 0x3f800000u); /* [1, 2) */
+  const int up = m >= 2.0f * 0.707106781186547524f; /* frexp's mantissa >= hm_logf's threshold */
+  m = up ? 0.5f * m : m; /* exact */
+  e += up;
+  const float x = m - 1.0f; /* exact (Sterbenz), in [-0.293, 0.415) */
+  const float z = x * x;
+  float y = hm_fma(hm_fma(hm_fma(7.0376836292E-2f, x, -1.1514610310E-1f), x, 1.1676998740E-1f),
+                   x, -1.2420140846E-1f);
+  y = hm_fma(hm_fma(hm_fma(y, x, 1.4249322787E-1f), x, -1.6668057665E-1f), x, 2.0000714765E-1f);
+  y = hm_fma(hm_fma(y, x, -2.4999993993E-1f), x, 3.3333331174E-1f);
+  y = y * x * z;
+  const float fe = (float)e;
+  y = hm_fma(-2.12194440e-4f, fe, y);
+  y = hm_fma(-0.5f, z, y);
+  const float lg = hm_fma(0.693359375f, fe, x + y); /* log b (b > 0 normal) */
+  const float t = p * lg;
+  const float tc = hm_minf(hm_maxf(t, -87.0f), 88.0f);
+  const float w = hm_fma(1.44269504088896341f, tc, 0.5f);
+  const float wt = (float)(int32_t)w;
+  const float n = (wt > w) ? wt - 1.0f : wt; /* hm_floorf(w), |w| < 2^23: in [-125, 127] */
+  float r = hm_fma(-n, 0.693359375f, tc);
+  r = hm_fma(n, 2.12194440e-4f, r);
+  const float r2 = r * r;
+  float q = hm_fma(hm_fma(1.9875691500E-4f, r, 1.3981999507E-3f), r, 8.3334519073E-3f);
+  q = hm_fma(hm_fma(hm_fma(q, r, 4.1665795894E-2f), r, 1.6666665459E-1f), r, 5.0000001201E-1f);
+  q = hm_fma(q, r2, r) + 1.0f;
+  float res = q * hm_bits2f((uint32_t)((int)n + 127) << 23);
+  res = t > 88.0f ? hm_bits2f(0x7f800000u) : res;
+  res = t < -87.0f ? 0.0f : res;
+  res = b == hm_bits2f(0x7f800000u) ? b : res;
+  res = b != b ? b : res;
+  return b > 0.0f ? res : (b == 0.0f ? 0.0f : res);
+}
+
 /* utils.wrap_to_pi: ((x + pi) % (2 pi)) - pi with Python's floored modulo.  The quotient is
  * taken with the reciprocal (a possible off-by-one next to a multiple of 2 pi is corrected
  * below). */

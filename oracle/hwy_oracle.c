@@ -249,7 +249,7 @@ static float idm_acceleration(const Road* r, int self, int ev, int fv) {
   float tsp = (ev == 0) ? 0.0f : e->target_speed; /* plain Vehicle has no target_speed */
   tsp = hm_clipf(tsp, 0.0f, r->cfg->speed_limit);
   float base = hm_maxf(e->speed, 0.0f) / hm_absf(hm_not_zero(tsp));
-  float acc = hm_fma(-COMFORT_ACC_MAX, hm_powf(base, r->v[self].delta), COMFORT_ACC_MAX);
+  float acc = hm_fma(-COMFORT_ACC_MAX, hm_powf_idm(base, r->v[self].delta), COMFORT_ACC_MAX);
   if (fv >= 0) {
     float d = lane_s(r->v[fv].x) - lane_s(e->x); /* lane_distance_to */
     float g = desired_gap(r, ev, fv) / hm_not_zero(d);
@@ -992,6 +992,7 @@ int hwyo_math(int op, const float* in, const float* in2, float* out, int n) {
       case 12: { float c_; hm_sincosf(x, &r, &c_); } break;
       case 13: { float s_; hm_sincosf(x, &s_, &r); } break;
       case 14: r = hm_tanf_sc(x); break;
+      case 15: r = hm_powf_idm(x, y); break;
       default: return -1;
     }
     out[i] = r;

@@ -25,11 +25,15 @@ def _inputs(op, rng, n=200000):
         x = np.abs(rng.normal(0, 100, n)) + 1e-30
     elif op == 7:
         x = np.abs(rng.uniform(0, 4000, n))
+    elif op == 15:  # the IDM pow: base >= 0 over every binary32 exponent
+        x = (rng.uniform(1, 2, n) * np.exp2(rng.integers(-149, 128, n).astype(np.float64)))
     else:
         x = rng.normal(0, 100, n)
     y = None
     if op == 7:
         y = rng.uniform(-4.5, 4.5, n)
+    if op == 15:
+        y = rng.uniform(3.5, 4.5, n)
     if op == 10:
         y = rng.normal(0, 10, n)
     # IEEE special values and range edges ride along with every op
@@ -37,11 +41,13 @@ def _inputs(op, rng, n=200000):
                    1.0, -1.0, 0.5, np.pi / 2, np.pi, 2 * np.pi], np.float32)
     x = np.concatenate([x, sp])
     if y is not None:
-        y = np.concatenate([y, np.full(sp.size, 3.0 if op == 10 else 2.0)])
+        y = np.concatenate([y, np.full(sp.size, {10: 3.0, 15: 4.0}.get(op, 2.0))])
+    if op == 15:  # the IDM base is >= 0 (or NaN)
+        x = np.where(np.signbit(x), -x, x)
     return x.astype(np.float32), None if y is None else y.astype(np.float32)
 
 
-@pytest.mark.parametrize("op", list(range(15)))
+@pytest.mark.parametrize("op", list(range(16)))
 def test_math_library_bit_exact(op):
     rng = np.random.default_rng(op)
     x, y = _inputs(op, rng)
