@@ -114,12 +114,6 @@ constexpr int kMaxRowS = 256;  // states dim bound of the fused path (LDS)
 //    groups of the current one;
 //  - kRingDC weight blocks in flight per wave in the compact-LDS row kernels.
 constexpr int kRingDC = 2;
-#ifndef HWY_RING_D2
-#define HWY_RING_D2 4  // A/B (round 5): ring depth when a wave owns <= 2 column tiles
-#endif
-#ifndef HWY_ROWS_XCD
-#define HWY_ROWS_XCD 0  // A/B (round 5): row tiles clustered by XCD for ppo_wgrad's slices
-#endif
 constexpr int kWgTM = 128, kWgTN = 64;          // ppo_wgrad output tile
 constexpr int kWgWaves = 8;                     // ppo_wgrad waves (2 per SIMD)
 constexpr int kWgPart = kWgTM * kWgTN + kWgTM;  // floats per partial tile (+ bias sums)
@@ -410,7 +404,7 @@ __host__ __device__ inline TileGeom tile_geom(int S, int H, int sb, int hb) {
 // ring depth of the row kernels for H (ppo_rows<H/64, NW>: 16-column tiles per wave TW)
 __host__ __device__ inline int rows_ring_depth(int H) {
   const int qh = H / 64, nw = (qh % 2 == 0) ? 8 : 4, tw = H / nw / 16;
-  return tw <= 2 ? HWY_RING_D2 : (tw <= 4 ? 4 : 2);  // weight blocks in flight per wave
+  return tw <= 4 ? 4 : 2;  // weight blocks in flight per wave (8 at H 256: slower, round 5)
 }
 __host__ __device__ inline void rows_blocks(int S, int H, int* sb, int* hb) {
   const int D = rows_ring_depth(H);
@@ -824,15 +818,7 @@ struct RowArgs {
   int HP;
   float eps_clip, value_coef, entropy_coef;
   int32_t* counters;
-  int xgrp;  // > 1: row tiles clustered by workgroup id mod xgrp (row_tile_of)
 };
-
-// The row tile of workgroup b of n.  xgrp > 1 (and n % xgrp == 0): workgroups b = xgrp k + z take
-// tiles z n / xgrp + k, so under round-robin placement the tiles of ppo_wgrad's row slice z are
-// produced on the XCD that reads them (speed only; the results do not depend on placement).
-__device__ __forceinline__ int row_tile_of(int b, int n, int xgrp) {
-  return (xgrp > 1 && n % xgrp == 0) ? (b % xgrp) * (n / xgrp) + b / xgrp : b;
-}
 
 // Row pitch (floats) of the row kernels' LDS images for n columns (n % 16 == 0): n + 8, i.e. a
 // quad pitch = 2 mod 4.  The MFMA operand reads (ds_read_b128, lane (g, c) reads quad
@@ -970,7 +956,7 @@ __device__ __forceinline__ void zero_acc(f32x4 (&acc)[RB][TW]) {
 }
 
 template <int TW>
-constexpr int ring_depth() { return TW <= 2 ? HWY_RING_D2 : (TW <= 4 ? 4 : 2); }
+constexpr int ring_depth() { return TW <= 4 ? 4 : 2; }
 
 // segment table of the row kernels: forward W1, W2, Wa1, Wc1 ([N][K]); backward Wa1, Wc1, W2
 // read k-major for dh2 = dac [Wa1; Wc1] and dh1 = dh2 W2.  With a tile image (TileGeom; kept by
@@ -1308,7 +1294,7 @@ __device__ __forceinline__ void rows_body(const RowArgs& r) {
   PSEC_DECL
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int S = r.S;
-  const int tile = row_tile_of(blockIdx.x, gridDim.x, r.xgrp);
+  const int tile = blockIdx.x;
   const int row0 = tile * RT;
   const int nrows = min(RT, r.B - row0);
   const float* P = r.params;
@@ -2605,8 +2591,6 @@ static int forward_backward_k(const hwy_ppo_args* a, void* stream, int mask) {
     r.head_part = w.head_part, r.HP = w.HP;
     r.eps_clip = a->eps_clip, r.value_coef = a->value_coef, r.entropy_coef = a->entropy_coef;
     r.counters = a->counters;
-    // wgrad's row slices one per XCD: the row tiles of slice z made on the XCD that reads them
-    r.xgrp = (HWY_ROWS_XCD && w.split == chip_geom().xcds) ? w.split : 0;
     // 8 waves (2 per SIMD) when the columns split into 16-wide tiles, else 4
     const dim3 g1(w.n1), b4(256), b8(512), blk(256);
     if (!(mask & 1)) {

@@ -1,6 +1,6 @@
 set -o pipefail
 # round-5 A/B: product (pre-gathered rows) vs XCD-clustered row tiles vs ring depth 8 (16-row tiles)
-MODE=ppo VARS="xcd d8" TESTS=1 SHAPES="256:4096:60 256:16384:60" REPS=3 bash tools/ab.sh > gpurun_out/ab1_ppo.log 2>&1 || { tail -20 gpurun_out/ab1_ppo.log; exit 1; }
+MODE=ppo VARS="xcd d8" SHAPES="256:4096:60 256:16384:60" REPS=3 bash tools/ab.sh > gpurun_out/ab1_ppo.log 2>&1 || { tail -20 gpurun_out/ab1_ppo.log; exit 1; }
 cat gpurun_out/ab1_ppo.log
 MODE=kt VARS="xcd d8" MB=4096 REPS=1 bash tools/ab.sh > gpurun_out/ab1_kt.log 2>&1 || { tail -20 gpurun_out/ab1_kt.log; exit 1; }
 cat gpurun_out/ab1_kt.log
