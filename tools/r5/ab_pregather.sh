@@ -17,3 +17,6 @@ for pg in 1 0; do
   echo "== pregather $pg (4096 rows)"
   python3 $R/tools/summarize_stats.py "$(find $d -name '*kernel_stats.csv' | head -1)" 6
 done
+# then the first cells of the pre-registered intermediate recipe (profiles/r5/reward/PREREGISTERED.md)
+cd $R
+PART=B CELLS="sorted:256" bash tools/r5/reward_r5.sh
