@@ -453,7 +453,6 @@ struct Work {
   float *wg_slab;            // fused: [ntile][split][kWgPart] partial tiles
   float *xg;                 // fused: [B][S] gathered states
   float *wtile;              // fused: weight tile image (TileGeom)
-  float *hin;                // fused: [B][8] pre-gathered head inputs (kHin), next to xg
   int nhead, HP, sa, s2, s1, ca, c2, c1, nred;
   // fused path (ppo_rows + ppo_wgrad)
   bool fused;
@@ -614,18 +613,17 @@ inline Work carve(const hwy_ppo_dims& d, void* ws, int64_t* bytes_out) {
   const int64_t xg_n = w.fused ? (int64_t)B * S : 0;
   rows_blocks(S, H, &w.sb, &w.hb);
   const int64_t tile_n = w.fused ? tile_geom(S, H, w.sb, w.hb).total : 0;
-  const int64_t hin_n = w.fused ? (int64_t)B * 8 : 0;
-  int64_t sizes[18] = {
+  int64_t sizes[17] = {
       (int64_t)B * H, (int64_t)B * H, (int64_t)B * 2 * H, (int64_t)B * 2 * H, (int64_t)B * H,
       (int64_t)B * H, head_rows * w.HP, sa * 2 * H * H, sa * 2 * H,
       s2 * H * H, s2 * H, s1 * H * S, s1 * H,
-      norm_n, wg_slab_n, xg_n, tile_n, hin_n};
+      norm_n, wg_slab_n, xg_n, tile_n};
   float* p = (float*)ws;
-  float** dst[18] = {&w.h1, &w.h2, &w.ac, &w.dac, &w.dh2, &w.dh1, &w.head_part, &w.slab_ac,
+  float** dst[17] = {&w.h1, &w.h2, &w.ac, &w.dac, &w.dh2, &w.dh1, &w.head_part, &w.slab_ac,
                      &w.bias_ac, &w.slab_2, &w.bias_2, &w.slab_1, &w.bias_1, &w.norm_part,
-                     &w.wg_slab, &w.xg, &w.wtile, &w.hin};
+                     &w.wg_slab, &w.xg, &w.wtile};
   int64_t total = 0;
-  for (int i = 0; i < 18; ++i) {
+  for (int i = 0; i < 17; ++i) {
     int64_t n = (sizes[i] + 63) / 64 * 64;  // 256-B aligned sub-buffers
     if (p) *dst[i] = p + total;
     total += n;
@@ -811,8 +809,6 @@ struct RowArgs {
   int64_t off[13];
   float *h1, *h2, *dac, *dh2, *dh1;
   float* xg;         // [B][S] gathered states (ppo_wgrad's dW1 operand)
-  const float* hin;  // [B][8] pre-gathered head inputs (pre)
-  int pre;           // xg / hin already hold this minibatch's rows (hwy_ppo_args.pregathered)
   const float* tiles;  // weight tile image (TileGeom), in sync with params
   float* head_part;  // [gridDim.x][HP], one row per row tile
   int HP;
@@ -1309,32 +1305,20 @@ __device__ __forceinline__ void rows_body(const RowArgs& r) {
   const int hl = min(RPW * w + min(lane, RPW - 1), nrows - 1);
   float hz0, hz1, hold, hadv, hret, hq0, hq1;
   Gathered<RT, NT> xpre;
-  if (r.pre) {
-    // pre-gathered by the previous step's ppo_adam (or hwy_ppo_pregather): contiguous rows, no
-    // dependent index load; the squash corrections come with the head inputs (hin, kHin)
-    gather_issue<RT, NT>(r.xg, nullptr, S, nrows, row0, H, xpre);
-    const f32x4 ha = *reinterpret_cast<const f32x4*>(r.hin + (long)(row0 + hl) * 8);
-    const f32x4 hb = *reinterpret_cast<const f32x4*>(r.hin + (long)(row0 + hl) * 8 + 4);
-    hz0 = ha[0], hz1 = ha[1], hold = ha[2], hadv = ha[3];
-    hret = hb[0], hq0 = hb[1], hq1 = hb[2];
-  } else {
-    const long hsrc = (long)r.idx[row0 + hl];
-    gather_issue<RT, NT>(r.states, r.idx, S, nrows, row0, H, xpre);
-    hz0 = r.pre_tanh[hsrc * 2];
-    hz1 = r.pre_tanh[hsrc * 2 + 1];
-    hold = r.old_logp[hsrc];
-    hadv = r.adv[hsrc];
-    hret = r.ret[hsrc];
-  }
+  const long hsrc = (long)r.idx[row0 + hl];
+  gather_issue<RT, NT>(r.states, r.idx, S, nrows, row0, H, xpre);
+  hz0 = r.pre_tanh[hsrc * 2];
+  hz1 = r.pre_tanh[hsrc * 2 + 1];
+  hold = r.old_logp[hsrc];
+  hadv = r.adv[hsrc];
+  hret = r.ret[hsrc];
   R.prime();
   const int nb = w * (H / NW);  // this wave's output columns of an H-wide layer
   f32x4 acc[RB][TW];
   // the squash correction depends on the stored pre-tanh actions only: computed here, its
   // latency hides behind the forward instead of lengthening the loss head's dependent chain
-  if (!r.pre) {
-    hq0 = squash_corr(hz0);
-    hq1 = squash_corr(hz1);
-  }
+  hq0 = squash_corr(hz0);
+  hq1 = squash_corr(hz1);
   float wa0[TW], wa1[TW], wc[TW];
 #pragma unroll
   for (int u = 0; u < TW; ++u) {
@@ -1353,7 +1337,7 @@ __device__ __forceinline__ void rows_body(const RowArgs& r) {
   f32x4 av[RB][TW], cv[RB][TW];  // a1, c1 of this wave's columns (C layout)
   uint32_t mb[2] = {0u, 0u};      // CMP: ReLU decisions of h1, h2 (this lane's C elements)
   rows_forward<QH, NW, RT, true, D, 7, true, CMP>(R, r.states, r.idx, S, nrows, row0, P, r.off, X,
-                                                  H1, P1, AC, r.pre ? nullptr : r.xg, r.h1,
+                                                  H1, P1, AC, r.xg, r.h1,
                                                   r.h2, mb, av,
                                                   cv PSEC_ARGS, &xpre);
   PSEC(3);
@@ -2243,92 +2227,7 @@ __global__ void __launch_bounds__(kRedThreads) ppo_reduce(RedArgs r) {
 }
 
 // entropy & total loss need the actor/critic means: second tiny pass by the optimizer kernel
-// The pre-gather of one minibatch's rows (hwy_ppo_args.next_idx, hwy_ppo_pregather): workgroup
-// b of n takes rows [b rpw, (b + 1) rpw), rpw = ceil(B / n).  xg[row] = states[idx[row]] (float4
-// pieces), hin[row] = {z0, z1, old_logp, adv, ret, squash_corr(z0), squash_corr(z1), 0} (kHin).
-struct GatherArgs {
-  const int64_t* idx;  // null: off
-  const float *states, *pre_tanh, *old_logp, *adv, *ret;
-  float *xg, *hin;
-  int B, S;
-};
-constexpr int kPgMax = 8;  // float4 pieces per thread held across the Adam update (more: looped)
-struct PreGather {
-  int r0, r1, items;
-  int64_t src[kPgMax];
-  f32x4 v[kPgMax];
-  int64_t hsrc;
-  f32x4 ha, hb;
-};
-// (1) the index loads, issued first (vector memory completes in issue order)
-__device__ __forceinline__ void pregather_begin(const GatherArgs& g, int wg, int nwg, PreGather& p) {
-  const int rpw = (g.B + nwg - 1) / nwg;
-  p.r0 = min(g.B, wg * rpw);
-  p.r1 = min(g.B, p.r0 + rpw);
-  const int q4 = g.S / 4;
-  p.items = (p.r1 - p.r0) * q4;
-#pragma unroll
-  for (int i = 0; i < kPgMax; ++i) {
-    const int e = (int)threadIdx.x + i * (int)blockDim.x;
-    p.src[i] = e < p.items ? g.idx[p.r0 + e / q4] : 0;
-  }
-  const int hr = p.r0 + (int)threadIdx.x;
-  p.hsrc = hr < p.r1 ? g.idx[hr] : 0;
-}
-// (2) the rows they name (waits for the index loads only; later loads stay in flight)
-__device__ __forceinline__ void pregather_loads(const GatherArgs& g, PreGather& p) {
-  const int q4 = g.S / 4;
-#pragma unroll
-  for (int i = 0; i < kPgMax; ++i) {
-    const int e = (int)threadIdx.x + i * (int)blockDim.x;
-    if (e < p.items) p.v[i] = *reinterpret_cast<const f32x4*>(g.states + p.src[i] * g.S + 4 * (e % q4));
-  }
-  if (p.r0 + (int)threadIdx.x < p.r1) {
-    const int64_t q = p.hsrc;
-    p.ha = f32x4{g.pre_tanh[2 * q], g.pre_tanh[2 * q + 1], g.old_logp[q], g.adv[q]};
-    p.hb = f32x4{g.ret[q], 0.0f, 0.0f, 0.0f};
-  }
-}
-// (3) the stores (and the pieces past kPgMax per thread, loaded and stored here)
-__device__ __forceinline__ void pregather_store(const GatherArgs& g, const PreGather& p) {
-  const int q4 = g.S / 4;
-#pragma unroll
-  for (int i = 0; i < kPgMax; ++i) {
-    const int e = (int)threadIdx.x + i * (int)blockDim.x;
-    if (e < p.items)
-      *reinterpret_cast<f32x4*>(g.xg + (long)(p.r0 + e / q4) * g.S + 4 * (e % q4)) = p.v[i];
-  }
-  for (int e = (int)threadIdx.x + kPgMax * (int)blockDim.x; e < p.items; e += blockDim.x) {
-    const int row = p.r0 + e / q4, k = 4 * (e % q4);
-    *reinterpret_cast<f32x4*>(g.xg + (long)row * g.S + k) =
-        *reinterpret_cast<const f32x4*>(g.states + g.idx[row] * g.S + k);
-  }
-  const int hr = p.r0 + (int)threadIdx.x;
-  if (hr < p.r1) {
-    f32x4 hb = p.hb;
-    hb[1] = squash_corr(p.ha[0]);
-    hb[2] = squash_corr(p.ha[1]);
-    *reinterpret_cast<f32x4*>(g.hin + (long)hr * 8) = p.ha;
-    *reinterpret_cast<f32x4*>(g.hin + (long)hr * 8 + 4) = hb;
-  }
-  for (int row = hr + (int)blockDim.x; row < p.r1; row += blockDim.x) {  // rpw > blockDim
-    const int64_t q = g.idx[row];
-    const float z0 = g.pre_tanh[2 * q], z1 = g.pre_tanh[2 * q + 1];
-    *reinterpret_cast<f32x4*>(g.hin + (long)row * 8) = f32x4{z0, z1, g.old_logp[q], g.adv[q]};
-    *reinterpret_cast<f32x4*>(g.hin + (long)row * 8 + 4) =
-        f32x4{g.ret[q], squash_corr(z0), squash_corr(z1), 0.0f};
-  }
-}
-
-__global__ void __launch_bounds__(256) ppo_pregather(GatherArgs g) {
-  PreGather p;
-  pregather_begin(g, blockIdx.x, gridDim.x, p);
-  pregather_loads(g, p);
-  pregather_store(g, p);
-}
-
 struct OptArgs {
-  GatherArgs g;  // the next minibatch's pre-gather (g.idx null: none)
   float* params;
   const float* grads;
   float* m;
@@ -2482,10 +2381,6 @@ __device__ __forceinline__ void adam_elem(const OptArgs& o, int64_t i, float g_r
 __global__ void __launch_bounds__(256) ppo_adam(OptArgs o) {
   __shared__ float red[4];
   __shared__ float sh[3];
-  // the next minibatch's pre-gather: its index loads first, its rows after this kernel's own
-  // loads, its stores last -- off the clip coefficient's chain
-  PreGather pg;
-  if (o.g.idx) pregather_begin(o.g, blockIdx.x, gridDim.x, pg);
   // the norm partial and the step count first (the clip coefficient's chain waits on them), then
   // this thread's elements (256 apart, coalesced), whose loads overlap the norm reduction
   const float first = (int)threadIdx.x < o.nred ? o.norm_part[threadIdx.x] : 0.0f;
@@ -2497,7 +2392,6 @@ __global__ void __launch_bounds__(256) ppo_adam(OptArgs o) {
     const int64_t ii = i < o.numel ? i : 0;
     g_raw[q] = o.grads[ii], m_old[q] = o.m[ii], v_old[q] = o.v[ii], p_old[q] = o.params[ii];
   }
-  if (o.g.idx) pregather_loads(o.g, pg);
   adam_scalars(o, red, sh, first, step);
 #pragma unroll
   for (int q = 0; q < kAdamEPT; ++q) {
@@ -2505,7 +2399,6 @@ __global__ void __launch_bounds__(256) ppo_adam(OptArgs o) {
     if (i >= o.numel) break;
     adam_elem(o, i, g_raw[q], m_old[q], v_old[q], p_old[q], sh);
   }
-  if (o.g.idx) pregather_store(o.g, pg);
 }
 
 template <int AM, int BM, int EPI>
@@ -2526,17 +2419,6 @@ int launch_gemm(const GemmArgs& g, int splits, hipStream_t s) {
 GemmArgs gemm_args() {
   GemmArgs g = {};
   g.split = 1 << 30;
-  return g;
-}
-
-// the pre-gather of minibatch rows idx into the workspace's xg / hin
-GatherArgs gather_args(const hwy_ppo_args* a, const Work& w, const int64_t* idx) {
-  GatherArgs g = {};
-  g.idx = idx;
-  g.states = a->states, g.pre_tanh = a->pre_tanh, g.old_logp = a->old_logp;
-  g.adv = a->adv, g.ret = a->ret;
-  g.xg = w.xg, g.hin = w.hin;
-  g.B = a->dims.B, g.S = a->dims.S;
   return g;
 }
 
@@ -2586,7 +2468,6 @@ static int forward_backward_k(const hwy_ppo_args* a, void* stream, int mask) {
     r.adv = a->adv, r.ret = a->ret, r.params = P;
     for (int i = 0; i < 13; ++i) r.off[i] = L.off[i];
     r.h1 = w.h1, r.h2 = w.h2, r.dac = w.dac, r.dh2 = w.dh2, r.dh1 = w.dh1, r.xg = w.xg;
-    r.hin = w.hin, r.pre = a->pregathered ? 1 : 0;
     r.tiles = w.wtile;
     r.head_part = w.head_part, r.HP = w.HP;
     r.eps_clip = a->eps_clip, r.value_coef = a->value_coef, r.entropy_coef = a->entropy_coef;
@@ -2776,8 +2657,6 @@ int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream) {
   o.nred = (w.fused && !a->grads_modified) ? w.nred2 : w.nred;
   o.lr = a->lr, o.beta1 = a->beta1, o.beta2 = a->beta2, o.eps = a->adam_eps;
   o.max_norm = a->max_grad_norm;
-  if (w.fused && a->next_idx)  // the next minibatch's rows, gathered while Adam runs
-    o.g = gather_args(a, w, a->next_idx);
   if (w.fused) {
     o.tiles = w.wtile;
     o.o_w1 = L.off[P_W1], o.o_w2 = L.off[P_W2], o.o_wa1 = L.off[P_WA1], o.o_wc1 = L.off[P_WC1];
@@ -2785,14 +2664,6 @@ int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream) {
   }
   const int nadam = (int)((L.numel + 256 * kAdamEPT - 1) / (256 * kAdamEPT));
   hipLaunchKernelGGL(ppo_adam, dim3(nadam), dim3(256), 0, s, o);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-int hwy_ppo_pregather(const hwy_ppo_args* a, void* stream) {
-  if (!a || !a->idx || hwy_ppo_workspace_bytes(&a->dims) < 0 || !fused_ok(a->dims)) return -1;
-  const Work w = carve(a->dims, a->workspace, nullptr);
-  const GatherArgs g = gather_args(a, w, a->idx);
-  hipLaunchKernelGGL(ppo_pregather, dim3((a->dims.B + 15) / 16), dim3(256), 0, (hipStream_t)stream, g);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -43,7 +43,6 @@ class PpoArgs(ctypes.Structure):
         ("entropy_coef", ctypes.c_float), ("max_grad_norm", ctypes.c_float),
         ("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
         ("adam_eps", ctypes.c_float), ("grads_modified", ctypes.c_int32),
-        ("next_idx", ctypes.c_void_p), ("pregathered", ctypes.c_int32),
     ]
 
 
@@ -68,8 +67,6 @@ def _bind(L):
     L.hwy_ppo_optimizer.argtypes = [ctypes.POINTER(PpoArgs), ctypes.c_void_p]
     L.hwy_ppo_optimizer.restype = ctypes.c_int
     L.hwy_ppo_sync_params.argtypes = [ctypes.POINTER(PpoArgs), ctypes.c_void_p]
-    L.hwy_ppo_pregather.argtypes = [ctypes.POINTER(PpoArgs), ctypes.c_void_p]
-    L.hwy_ppo_pregather.restype = ctypes.c_int
     L.hwy_ppo_sync_params.restype = ctypes.c_int
     L.hwy_ppo_act.argtypes = [ctypes.POINTER(PpoActArgs), ctypes.c_void_p]
     L.hwy_ppo_act.restype = ctypes.c_int
@@ -271,9 +268,6 @@ class FusedPPO:
         self.capture_collectives = self._rccl and os.environ.get("HWY_GRAPH_COLLECTIVES", "1") != "0"
         self._captured_collectives = False
         self.use_graphs = use_graphs
-        # rows pre-gathered by the previous step's optimizer (hwy_ppo_args.next_idx); False:
-        # every row kernel gathers its rows through the minibatch indices (same bits)
-        self.pregather = True
         self._import_torch_state()
         self._graphs = None
         self._bound_key = None
@@ -406,23 +400,14 @@ class FusedPPO:
         # the captured graphs bake in the buffer addresses and the scalar hyper-parameters of
         # PpoArgs: a change to either (an lr schedule, agent.eps_clip, ...) forces a recapture
         key = (states.data_ptr(), pre_tanh.data_ptr(), old_lp.data_ptr(), adv.data_ptr(),
-               ret.data_ptr(), perm.data_ptr(), self.pregather) + self._scalar_key()
+               ret.data_ptr(), perm.data_ptr()) + self._scalar_key()
         args = [self._args(states, pre_tanh, old_lp, adv, ret, perm.data_ptr() + i * mb * 8)
                 for i in range(nmb)]
-        # each step's optimizer gathers the next minibatch's rows (the last step: the next
-        # epoch's first), so every row kernel reads its rows pre-gathered (hwy_ppo_args.next_idx)
-        if self.pregather:
-            for i, a in enumerate(args):
-                a.next_idx = perm.data_ptr() + ((i + 1) % nmb) * mb * 8
-                a.pregathered = 1
         self._last_args = args
         self.counters[1].zero_()
         # the weight tile image the row kernel streams: params may have been written since the
         # last update (checkpoint load, torch optimizer); hwy_ppo_optimizer keeps it in step
         self.sync_params(args[0])
-        if self.pregather:
-            check(self.L.hwy_ppo_pregather(ctypes.byref(args[0]), stream_ptr()),
-                  "hwy_ppo_pregather")
         if not self.use_graphs:
             for _ in range(epochs):
                 for a in args:

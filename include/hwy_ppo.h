@@ -66,16 +66,6 @@ typedef struct hwy_ppo_args {
   float lr, beta1, beta2, adam_eps;
   int32_t grads_modified; /* grads changed after forward_backward (e.g. all-reduced): the
                              optimizer recomputes the gradient norm from them */
-  /* Pre-gathered minibatch rows (fused path; NULL / 0 = off).  The row kernel's first act is a
-   * dependent gather (idx, then the states rows it names, the stored actions, log-probs,
-   * advantages and returns); it sits on the minibatch step's critical path.  With next_idx set,
-   * hwy_ppo_optimizer also gathers the NEXT minibatch's rows (next_idx[dims.B]) into the
-   * workspace while its Adam update runs, and a forward_backward with pregathered = 1 reads its
-   * rows from there (contiguous) instead of through idx.  The workspace holds one gathered
-   * minibatch: a step's optimizer overwrites it only after that step's kernels have read it.
-   * Start a chain with hwy_ppo_pregather on the first minibatch. */
-  const int64_t* next_idx;
-  int32_t pregathered;
 } hwy_ppo_args;
 
 /* Forward, loss, backward: writes grads (flat) and the metrics row. */
@@ -90,9 +80,6 @@ int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream);
  * `stream` first; synchronous, not graph-capturable; fused path, grads_modified == 0.
  * -1 bad args, -2 HIP error. */
 int hwy_ppo_time_kernels(const hwy_ppo_args* a, void* stream, int reps, float* us);
-/* Gather the minibatch rows of a->idx into the workspace (what hwy_ppo_optimizer does for
- * next_idx), for a following forward_backward with pregathered = 1.  Fused path only. */
-int hwy_ppo_pregather(const hwy_ppo_args* a, void* stream);
 /* Rebuild the workspace's weight tile image from params (uses dims, params, workspace). */
 int hwy_ppo_sync_params(const hwy_ppo_args* a, void* stream);
 

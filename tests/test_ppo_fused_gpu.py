@@ -669,31 +669,3 @@ def test_act_after_graph_replayed_reference_updates():
             got = fused_act(ag, x, deterministic=True)
         for r, g in zip(ref, got):
             torch.testing.assert_close(g, r, rtol=1e-4, atol=2e-5)
-
-
-@pytest.mark.parametrize("S,H,n,nmb,graphs", [(60, 256, 16384, 4, True), (60, 256, 8192, 2, False),
-                                              (120, 256, 4096, 4, True), (60, 64, 2048, 4, True),
-                                              (240, 512, 4096, 2, False)])
-def test_pregathered_rows_equal_the_indexed_gather(S, H, n, nmb, graphs):
-    """Each step's ppo_adam gathers the next minibatch's rows (hwy_ppo_args.next_idx; the first
-    minibatch by hwy_ppo_pregather), so the row kernel reads them contiguous instead of through
-    the indices.  An update through that path leaves the same weights, Adam moments and metrics,
-    bit for bit, as one whose row kernels gather through idx (FusedPPO.pregather = False), at the
-    16-, 32- and 64-row tiles and over epochs (the last step gathers the next epoch's first)."""
-    a, b = _agents(S, H, epochs=3, graphs=graphs)
-    _, c = _agents(S, H, epochs=3, graphs=graphs)
-    s, z, lp, adv, ret, perm = _data(n, S, a)
-    Fb = FusedPPO(b, n // nmb, nmb, use_graphs=graphs)
-    Fc = FusedPPO(c, n // nmb, nmb, use_graphs=graphs)
-    Fc.pregather = False
-    mb_ = Fb.run(s, z, lp, adv.clone(), ret.clone(), perm.clone())
-    mc_ = Fc.run(s, z, lp, adv.clone(), ret.clone(), perm.clone())
-    torch.cuda.synchronize()
-    assert torch.equal(Fb.flat, Fc.flat) and torch.equal(Fb.m, Fc.m) and torch.equal(Fb.v, Fc.v)
-    assert torch.equal(mb_, mc_)
-    # a second update on new rows (the pre-gather chain restarts from the new first minibatch)
-    s2, z2, lp2, adv2, ret2, perm2 = _data(n, S, a, seed=7)
-    Fb.run(s2, z2, lp2, adv2.clone(), ret2.clone(), perm2.clone())
-    Fc.run(s2, z2, lp2, adv2.clone(), ret2.clone(), perm2.clone())
-    torch.cuda.synchronize()
-    assert torch.equal(Fb.flat, Fc.flat)

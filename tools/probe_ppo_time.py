@@ -27,7 +27,6 @@ adv = torch.randn(n, device=dev)
 ret = torch.randn(n, device=dev)
 perm = torch.randperm(n, device=dev)
 F = FusedPPO(ag, mb, nmb, use_graphs=True)
-F.pregather = os.environ.get("HWY_PREGATHER", "1") != "0"  # A/B: rows pre-gathered by ppo_adam
 F.run(s, z, lp, adv, ret, perm)
 torch.cuda.synchronize()
 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
