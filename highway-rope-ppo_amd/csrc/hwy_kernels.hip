@@ -230,7 +230,11 @@ __device__ __forceinline__ float idm_free(float ev_spd, float ev_tsp, float delt
   float base = hm_maxf(ev_spd, 0.0f) / hm_absf(hm_not_zero(tsp));
   if (kSkip & 32) return hm_fma(-COMFORT_ACC_MAX, base * base, COMFORT_ACC_MAX);
   // np.power(base, DELTA): hm_powf's arithmetic, branch-free (bit-identical, hwy_math.h)
+#ifdef HWY_AB_OLD_POW  // A/B (round 5, temporary)
+  return hm_fma(-COMFORT_ACC_MAX, hm_powf(base, delta), COMFORT_ACC_MAX);
+#else
   return hm_fma(-COMFORT_ACC_MAX, hm_powf_idm(base, delta), COMFORT_ACC_MAX);
+#endif
 }
 
 // IDMVehicle.acceleration given its free-road term `acc` (interaction with the front vehicle)
