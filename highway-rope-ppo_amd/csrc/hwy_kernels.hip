@@ -1084,13 +1084,31 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
                 vb = shf(v.spd, b);
     // exact pre-check (are_polygons_intersecting is only called inside it), then the SAT test
     const float dx = xb - xa, dy = yb - ya;
-    const bool pass = has && !(__builtin_sqrtf(hm_fma(dx, dx, dy * dy)) >
-                               (VEH_DIAGONAL + VEH_DIAGONAL) / 2.0f + va * dt);
+    bool pass = has && !(__builtin_sqrtf(hm_fma(dx, dx, dy * dy)) >
+                         (VEH_DIAGONAL + VEH_DIAGONAL) / 2.0f + va * dt);
     if (!wave_any(pass)) continue;
+    const float dax = (va * ca) * dt, day = (va * sa) * dt, dbx = (vb * cb) * dt, dby = (vb * sb) * dt;
+#ifndef HWY_AB_NO_SATPRE  // A/B (round 5, temporary)
+    // a's v axis (the SAT's second edge normal) first: a pair separated on it both as it stands
+    // and swept by the velocities ends with intersecting = will_intersect = false and no
+    // translation whatever the other axes give (the SAT only ever clears the two flags), so it
+    // leaves the round; rounds whose pairs all leave skip the SAT (cars side by side in adjacent
+    // lanes).  The same operations as sat_collide's edge 1, so the decision is exact.
+    {
+      float a0, a1, b0, b1;
+      rect_interval(xa, ya, ca, sa, -sa, ca, a0, a1);
+      rect_interval(xb, yb, cb, sb, -sa, ca, b0, b1);
+      const float vp = hm_fma(-sa, dax - dbx, ca * (day - dby));
+      const bool sep = interval_distance(a0, a1, b0, b1) > 0.0f &&
+                       interval_distance(vp < 0.0f ? a0 + vp : a0, vp < 0.0f ? a1 : a1 + vp, b0,
+                                         b1) > 0.0f;
+      pass = pass && !sep;
+      if (!wave_any(pass)) continue;
+    }
+#endif
     bool inter, will;
     float tx, ty;
-    sat_collide(pass, xa, ya, ca, sa, (va * ca) * dt, (va * sa) * dt, xb, yb, cb, sb, (vb * cb) * dt,
-                (vb * sb) * dt, &inter, &will, &tx, &ty);
+    sat_collide(pass, xa, ya, ca, sa, dax, day, xb, yb, cb, sb, dbx, dby, &inter, &will, &tx, &ty);
     if (pass && will) {
       atomicMax(&cl.imx[a], ((uint64_t)(b + 1) << 32) | hm_f2bits(tx / 2.0f));
       atomicMax(&cl.imy[a], ((uint64_t)(b + 1) << 32) | hm_f2bits(ty / 2.0f));
