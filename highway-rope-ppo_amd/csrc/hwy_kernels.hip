@@ -230,11 +230,7 @@ __device__ __forceinline__ float idm_free(float ev_spd, float ev_tsp, float delt
   float base = hm_maxf(ev_spd, 0.0f) / hm_absf(hm_not_zero(tsp));
   if (kSkip & 32) return hm_fma(-COMFORT_ACC_MAX, base * base, COMFORT_ACC_MAX);
   // np.power(base, DELTA): hm_powf's arithmetic, branch-free (bit-identical, hwy_math.h)
-#ifdef HWY_AB_OLD_POW  // A/B (round 5, temporary)
-  return hm_fma(-COMFORT_ACC_MAX, hm_powf(base, delta), COMFORT_ACC_MAX);
-#else
   return hm_fma(-COMFORT_ACC_MAX, hm_powf_idm(base, delta), COMFORT_ACC_MAX);
-#endif
 }
 
 // IDMVehicle.acceleration given its free-road term `acc` (interaction with the front vehicle)
@@ -1088,7 +1084,6 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
                          (VEH_DIAGONAL + VEH_DIAGONAL) / 2.0f + va * dt);
     if (!wave_any(pass)) continue;
     const float dax = (va * ca) * dt, day = (va * sa) * dt, dbx = (vb * cb) * dt, dby = (vb * sb) * dt;
-#ifndef HWY_AB_NO_SATPRE  // A/B (round 5, temporary)
     // a's v axis (the SAT's second edge normal) first: a pair separated on it both as it stands
     // and swept by the velocities ends with intersecting = will_intersect = false and no
     // translation whatever the other axes give (the SAT only ever clears the two flags), so it
@@ -1105,7 +1100,6 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
       pass = pass && !sep;
       if (!wave_any(pass)) continue;
     }
-#endif
     bool inter, will;
     float tx, ty;
     sat_collide(pass, xa, ya, ca, sa, dax, day, xb, yb, cb, sb, dbx, dby, &inter, &will, &tx, &ty);
