@@ -2242,6 +2242,7 @@ struct OptArgs {
   float* tiles;  // fused path: the weight tile image, rewritten with the new weights
   int64_t o_w1, o_w2, o_wa1, o_wc1;
   int S, H, sb, hb;
+  int skip;  // dev builds' pricing (HWY_PPO_SKIP, WRONG results): 1 no tile writes, 2 empty; 0
 };
 
 // float index of B[k][n] in a tile image region with nblk blocks per 16 columns
@@ -2381,6 +2382,8 @@ __device__ __forceinline__ void adam_elem(const OptArgs& o, int64_t i, float g_r
 }
 
 __global__ void __launch_bounds__(256) ppo_adam(OptArgs o) {
+  if (o.skip & 2) return;
+  if (o.skip & 1) o.tiles = nullptr;
   __shared__ float red[4];
   __shared__ float sh[3];
   // the norm partial and the step count first (the clip coefficient's chain waits on them), then
@@ -2664,6 +2667,7 @@ int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream) {
     o.o_w1 = L.off[P_W1], o.o_w2 = L.off[P_W2], o.o_wa1 = L.off[P_WA1], o.o_wc1 = L.off[P_WC1];
     o.S = d.S, o.H = d.H, o.sb = w.sb, o.hb = w.hb;
   }
+  o.skip = dev_knob_int("HWY_PPO_SKIP", 0) & 3;
   const int nadam = (int)((L.numel + 256 * kAdamEPT - 1) / (256 * kAdamEPT));
   hipLaunchKernelGGL(ppo_adam, dim3(nadam), dim3(256), 0, s, o);
   return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -197,7 +197,7 @@ def _check_grads(ga, gb, g64, msg=""):
 def test_fused_gradient_matches_autograd(S, H, mb):
     """One fused forward/backward against autograd on the same minibatch.  The reference
     gradient is float64 autograd: at S = 240 / H = 512 and 4096 rows torch's own fp32 GEMMs
-    are off by up to 1.7e-6 on near-cancelling sums (tools/r2/probe_grad_f64.py, where the
+    are off by up to 1.7e-6 on near-cancelling sums (tools/probe_grad_f64.py, where the
     fused kernel stays within 7e-10), so fp32 torch is no longer the tighter reference; at
     other shapes both fp32 results share the same rounding of the loss head and agree with
     each other better than with float64.  The fused gradient must agree elementwise with one

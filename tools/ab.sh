@@ -8,7 +8,7 @@
 #   MODE=step  VARS=... [TESTS=1] [ENVS="4096 16384"] [REPS=3]   hwy_step time (tools/probe_step.py)
 #   MODE=kt    VARS=... [WHAT=ppo|step] [MB=16384]   rocprofv3 kernel-trace averages per library
 #   MODE=pmc   VARS=... [COUNTERS="SQ_INSTS_VALU ..."]  SQ instruction counts per hwy_step launch
-#   MODE=act   VARS=... [ROWS="4096 16384 32768"]    ppo_act kernel-trace time (tools/r3/probe_act.py)
+#   MODE=act   VARS=... [ROWS="4096 16384 32768"]    ppo_act kernel-trace time (tools/probe_act.py)
 # TESTS=1 first runs the parity tests of the touched kernel on the product library and every
 # variant (tests/test_ppo_fused_gpu.py for ppo/act, tests/test_env_parity_gpu.py for step/pmc).
 set -o pipefail
@@ -57,7 +57,7 @@ kt|pmc|act)
         kt) if [ "${WHAT:-ppo}" = step ]; then prog="$R/tools/probe_step.py 4096"; rx=hwy_step
             else prog="$R/tools/probe_ppo_time.py 256 3 ${MB:-16384}"; rx=ppo_; fi
             prof="--kernel-trace --stats" ;;
-        act) prog="$R/tools/r3/probe_act.py ${ROWS:-4096 16384 32768}"; rx=ppo_act
+        act) prog="$R/tools/probe_act.py ${ROWS:-4096 16384 32768}"; rx=ppo_act
              prof="--kernel-trace --stats" ;;
         pmc) prog="$R/tools/probe_step.py 4096"; rx=hwy_step
              prof="--pmc ${COUNTERS:-SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_INSTS_LDS SQ_WAVES}" ;;

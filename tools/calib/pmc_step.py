@@ -1,5 +1,5 @@
 """Runs the calibration kernels (known bytes) and 40 hwy_step launches in one process, for
-rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/calib/pmc_step.sh, tools/r3/pmc_workload.sh).
+rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/calib/pmc_step.sh, tools/pmc_workload.sh).
 The workload is bench.py's --config (env PMC_CONFIG, default 1: 4096 envs x 15 observed, sorted;
 2: 16384 envs x 30 observed, shuffled + RoPE d 4; 4: 32768 envs x 30 observed, sorted), built
 through the reference's make_env exactly as bench.py builds it."""

@@ -6,7 +6,7 @@ the reference's batch_size-64 means of the same cells: each cell's mean and 95 %
 the cells on both sides, the Spearman rank correlation of the six means, and the one contrast the
 reference study is about, sorted h256 against the three PE conditions (Welch's t on the seeds).
 
-    python tools/r5/condition_order.py DIR E T [--out FILE]
+    python tools/condition_order.py DIR E T [--out FILE]
 DIR holds <condition>_h<H>_e<E>_t<T>/stats.json (e.g. profiles/r5/reward).
 """
 

@@ -7,7 +7,7 @@
 #              workload's minibatch (rows = E x T / 32) and state width S = N x F_out
 # -> profiles/hwy_step_pmc_E*_N*_F*.json, profiles/hwy_step_valu_E*_N*_F*.json,
 #    profiles/ppo_step_pmc_<rows>_S*_H*.json  (bench.py attaches them by those keys)
-#   CONFIG=2 bash tools/r3/pmc_workload.sh        (run from the repo root on the GPU box)
+#   CONFIG=2 bash tools/pmc_workload.sh        (run from the repo root on the GPU box)
 set -u
 R=$(pwd)
 C=${CONFIG:-2}

@@ -2,7 +2,7 @@
 HWY_LIB overrides the library."""
 import os, sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "highway-rope-ppo_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "highway-rope-ppo_amd"))
 import torch
 import hwy.native as native
 

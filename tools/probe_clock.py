@@ -3,7 +3,7 @@ VEXTRA=-DHWY_CLOCK_PROBE): s_memtime / s_memrealtime deltas per workgroup after 
 back-to-back minibatch steps (MI355X_MICROARCH.md, DVFS item 6).  probe_clock.py [rows] [seconds]"""
 import ctypes, os, sys, time
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "highway-rope-ppo_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "highway-rope-ppo_amd"))
 import torch
 import hwy.native as native
 

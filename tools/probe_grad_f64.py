@@ -1,6 +1,6 @@
 """Fused and torch-fp32 gradients against a float64 autograd reference (diagnostic)."""
 import sys, os, copy
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "highway-rope-ppo_amd"), os.path.join(ROOT, "tests")]
 import torch
 import torch.nn.functional as Fn

@@ -1,6 +1,6 @@
 """Times the fused PPO update (graph of ppo_rows / ppo_wgrad / ppo_wsum / ppo_adam) at the bench
 minibatch (development aid): probe_ppo_time.py [H] [reps] [minibatch rows] [S]; HWY_LIB
-overrides the library."""
+overrides the library; PROBE_KT=1 also prints each kernel's time (hwy_ppo_time_kernels)."""
 import os, sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "highway-rope-ppo_amd"))
@@ -36,6 +36,9 @@ for _ in range(reps):
 ev1.record()
 torch.cuda.synchronize()
 print(f"H={H}: {ev0.elapsed_time(ev1) / (reps * nmb) * 1e3:.1f} us per minibatch step", flush=True)
+if os.environ.get("PROBE_KT"):  # per-kernel times (hwy_ppo_time_kernels), after the timed loop
+    kt = F.time_kernels(16)
+    print("per kernel us: " + " ".join(f"{k} {v:.2f}" for k, v in kt.items()), flush=True)
 # bit-identity fingerprint of the final weights (variants that only reorder instructions must
 # print the same value as the product library)
 import hashlib
