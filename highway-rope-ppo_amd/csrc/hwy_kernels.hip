@@ -215,44 +215,36 @@ __device__ __forceinline__ int closest_lane(float y, int lanes) {
   return best;
 }
 
-// IDMVehicle.desired_gap(ego=a, front=b)
-__device__ __forceinline__ float desired_gap(float a_spd, float a_c, float a_s, float b_spd,
-                                             float b_c, float b_s) {
-  float avx = a_spd * a_c, avy = a_spd * a_s;
-  float bvx = b_spd * b_c, bvy = b_spd * b_s;
+// IDMVehicle.desired_gap(ego=a, front=b), from the velocity vectors (speed * (cos h, sin h),
+// formed once per vehicle and frame: the same products upstream's velocity property forms)
+__device__ __forceinline__ float desired_gap_v(float a_spd, float a_c, float a_s, float avx,
+                                               float avy, float bvx, float bvy) {
   float dv = hm_fma(avx - bvx, a_c, (avy - bvy) * a_s);
   return hm_fma(a_spd, TIME_WANTED, DISTANCE_WANTED) + (a_spd * dv) * INV_TWO_SQRT_AB;
 }
 
-// IDMVehicle.acceleration, free-road term (depends on the ego vehicle and DELTA only)
-__device__ __forceinline__ float idm_free(float ev_spd, float ev_tsp, float delta, float limit) {
+// IDMVehicle.acceleration, free-road term: the ego vehicle's base speed / target speed ...
+__device__ __forceinline__ float idm_base(float ev_spd, float ev_tsp, float limit) {
   float tsp = hm_clipf(ev_tsp, 0.0f, limit);
-  float base = hm_maxf(ev_spd, 0.0f) / hm_absf(hm_not_zero(tsp));
+  return hm_maxf(ev_spd, 0.0f) / hm_absf(hm_not_zero(tsp));
+}
+
+// ... raised to the deciding vehicle's DELTA, from the base and its log (hm_logf_idm):
+// np.power(base, DELTA) in hm_powf's arithmetic, branch-free (bit-identical, hwy_math.h)
+__device__ __forceinline__ float idm_free_from(float base, float lg, float delta) {
   if (kSkip & 32) return hm_fma(-COMFORT_ACC_MAX, base * base, COMFORT_ACC_MAX);
-  // np.power(base, DELTA): hm_powf's arithmetic, branch-free (bit-identical, hwy_math.h)
-  return hm_fma(-COMFORT_ACC_MAX, hm_powf_idm(base, delta), COMFORT_ACC_MAX);
+  return hm_fma(-COMFORT_ACC_MAX, hm_expf_idm(lg, delta, base), COMFORT_ACC_MAX);
 }
 
 // IDMVehicle.acceleration given its free-road term `acc` (interaction with the front vehicle)
+// (ev_vx, ev_vy, fv_vx, fv_vy: the two velocity vectors)
 __device__ __forceinline__ float idm_with_front(float acc, float ev_spd, float ev_x, float ev_c,
-                                                float ev_s, bool has_front, float fv_x,
-                                                float fv_spd, float fv_c, float fv_s) {
+                                                float ev_s, float ev_vx, float ev_vy,
+                                                bool has_front, float fv_x, float fv_vx,
+                                                float fv_vy) {
   if (has_front) {
     float d = fv_x - ev_x;
-    float g = desired_gap(ev_spd, ev_c, ev_s, fv_spd, fv_c, fv_s) / hm_not_zero(d);
-    acc = hm_fma(-COMFORT_ACC_MAX, g * g, acc);
-  }
-  return acc;
-}
-
-// IDMVehicle.acceleration(ego_vehicle=ev, front_vehicle=fv) with the caller's DELTA
-__device__ __forceinline__ float idm_acc(float ev_spd, float ev_tsp, float ev_x, float ev_c,
-                                         float ev_s, bool has_front, float fv_x, float fv_spd,
-                                         float fv_c, float fv_s, float delta, float limit) {
-  float acc = idm_free(ev_spd, ev_tsp, delta, limit);
-  if (has_front) {
-    float d = fv_x - ev_x;
-    float g = desired_gap(ev_spd, ev_c, ev_s, fv_spd, fv_c, fv_s) / hm_not_zero(d);
+    float g = desired_gap_v(ev_spd, ev_c, ev_s, ev_vx, ev_vy, fv_vx, fv_vy) / hm_not_zero(d);
     acc = hm_fma(-COMFORT_ACC_MAX, g * g, acc);
   }
   return acc;
@@ -844,33 +836,36 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   SEC(sp, 9);
   // position-space copies of the fronts' state (vehicle at position p on lane p), gathered
   // alongside the order so the fronts' values are one bpermute from their positions
-  const float xq = shf(v.x, ro.ord), spdq = shf(v.spd, ro.ord), cq = shf(ch, ro.ord),
-              sq = shf(sh, ro.ord);
+  // this vehicle's velocity vector (Vehicle.velocity), shared by every desired_gap of the frame
+  const float vvx = v.spd * ch, vvy = v.spd * sh;
+  const float xq = shf(v.x, ro.ord), vxq = shf(vvx, ro.ord), vyq = shf(vvy, ro.ord);
   int qfp[3];
   neighbours_ordered(C, lane, v, pres, ro, fi, ri, qfp);
   SEC(sp, 1);
 
   // gathers (all lanes active); a missing front reads this vehicle's own values (unused)
   const int sop = qfp[1];
-  const float op_x = shf(xq, sop), op_spd = shf(spdq, sop), op_c = shf(cq, sop),
-              op_s = shf(sq, sop);
-  float np_x[2], np_spd[2], np_c[2], np_s[2];
+  const float op_x = shf(xq, sop), op_vx = shf(vxq, sop), op_vy = shf(vyq, sop);
+  float np_x[2], np_vx[2], np_vy[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int a = qfp[2 * q];  // slot 0 (left, ln-1) and slot 2 (right, ln+1)
     np_x[q] = shf(xq, a);
-    np_spd[q] = shf(spdq, a);
-    np_c[q] = shf(cq, a);
-    np_s[q] = shf(sq, a);
+    np_vx[q] = shf(vxq, a);
+    np_vy[q] = shf(vyq, a);
   }
 
   // acceleration(self, front on own lane): IDM term and MOBIL's self_a
   float self_a = 0.0f;
   // (the free-road term is shared by every acceleration(self, .) evaluated this frame)
+  // every lane's free-road base and its log (the ego as a plain Vehicle: target speed 0), also
+  // read by mobil for a new follower (same base, the deciding vehicle's DELTA)
+  const float fbase = idm_base(v.spd, lane == 0 ? 0.0f : v.tsp, limit);
+  const float flog = hm_logf_idm(fbase);
   float a_free = 0.0f;
   if (actor) {
-    a_free = idm_free(v.spd, v.tsp, v.dlt, limit);
-    self_a = idm_with_front(a_free, v.spd, v.x, ch, sh, fi[1] >= 0, op_x, op_spd, op_c, op_s);
+    a_free = idm_free_from(fbase, flog, v.dlt);
+    self_a = idm_with_front(a_free, v.spd, v.x, ch, sh, vvx, vvy, fi[1] >= 0, op_x, op_vx, op_vy);
   }
 
   // IDMVehicle.change_lane_policy -> mobil, side lanes left then right (POLITENESS = 0, so the
@@ -891,8 +886,8 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
             v.x < ROAD_LENGTH + LANE_VEH_LEN))
         continue;  // is_reachable_from
       if (hm_absf(v.spd) < 1.0f) continue;
-      const float spa = idm_with_front(a_free, v.spd, v.x, ch, sh, fi[s] >= 0, np_x[q],
-                                       np_spd[q], np_c[q], np_s[q]);
+      const float spa = idm_with_front(a_free, v.spd, v.x, ch, sh, vvx, vvy, fi[s] >= 0, np_x[q],
+                                       np_vx[q], np_vy[q]);
       gain[q] = !((spa - self_a) < LANE_CHANGE_MIN_ACC_GAIN);
     }
   }
@@ -906,11 +901,11 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
       const int rq = q ? ri[2] : ri[0];
       const int b = rq >= 0 ? rq : lane;  // all lanes active: ds_bpermute
       const float nf_x = shf(v.x, b), nf_spd = shf(v.spd, b), nf_c = shf(ch, b), nf_s = shf(sh, b);
-      const float tsp_b = shf(v.tsp, b);
-      const float nf_tsp = (b == 0) ? 0.0f : tsp_b;  // plain Vehicle (ego) has no target_speed
+      const float nf_base = shf(fbase, b), nf_log = shf(flog, b);
       float nfp = 0.0f;
-      if (rq >= 0)
-        nfp = idm_acc(nf_spd, nf_tsp, nf_x, nf_c, nf_s, true, v.x, v.spd, ch, sh, v.dlt, limit);
+      if (rq >= 0)  // acceleration(ego_vehicle=new follower, front_vehicle=self), self's DELTA
+        nfp = idm_with_front(idm_free_from(nf_base, nf_log, v.dlt), nf_spd, nf_x, nf_c, nf_s,
+                             nf_spd * nf_c, nf_spd * nf_s, true, v.x, vvx, vvy);
       return !(nfp < -LANE_CHANGE_MAX_BRAKING_IMPOSED);
     };
     const int q1 = gain[1] ? 1 : 0;
@@ -944,7 +939,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
     if (!wave_any(cheap)) continue;
     const float xj = rdlf(v.x, j), vj = rdlf(v.spd, j), cj = rdlf(ch, j), sj = rdlf(sh, j);
     const float d = v.x - xj;
-    const float d_star = desired_gap(vj, cj, sj, v.spd, ch, sh);
+    const float d_star = desired_gap_v(vj, cj, sj, vj * cj, vj * sj, vvx, vvy);
     const bool cond = cheap && (0.0f < d) && (d < d_star);
     if (wave_any(cond) && lane == j) tl_cur = v.ln;
   }
@@ -962,14 +957,13 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
     if (extra) ft = fx;
   }
   const int st_ = ft >= 0 ? ft : lane;
-  const float ft_x = shf(v.x, st_), ft_spd = shf(v.spd, st_), ft_c = shf(ch, st_),
-              ft_s = shf(sh, st_);
+  const float ft_x = shf(v.x, st_), ft_vx = shf(vvx, st_), ft_vy = shf(vvy, st_);
   if (actor) {
     const float steer = (kSkip & 16) ? 0.0f : steering_tan(v.y, v.h, v.spd, v.tl);
     float acc = self_a;
     if (need_t) {
       const float acc_t =
-          idm_with_front(a_free, v.spd, v.x, ch, sh, ft >= 0, ft_x, ft_spd, ft_c, ft_s);
+          idm_with_front(a_free, v.spd, v.x, ch, sh, vvx, vvy, ft >= 0, ft_x, ft_vx, ft_vy);
       acc = hm_minf(acc, acc_t);
     }
     acc = hm_clipf(acc, -ACC_MAX, ACC_MAX);

@@ -311,7 +311,10 @@ HWY_HD float hm_powf(float b, float p) {
  * value above e^88 (3 (1 - b^p) rounds the same either way).  The same operations on the host and
  * on gfx950 (correctly rounded primitives, explicit fma): the oracle and the kernel agree bit for
  * bit. */
-HWY_HD float hm_powf_idm(float b, float p) {
+/* hm_powf_idm's two halves: log b, then exp(p log b) with its special-case selects on b.  One
+ * log serves every exponent applied to the same base (mobil's new follower: its own free-road
+ * base under the deciding vehicle's DELTA), and the composition is hm_powf_idm's arithmetic. */
+HWY_HD float hm_logf_idm(float b) {
   const uint32_t u = hm_f2bits(b);
   int e = (int)(u >> 23) - 127;
   float m = hm_bits2f((u & 0x007fffffu) | 0x3f800000u); /* [1, 2) */
@@ -328,7 +331,10 @@ HWY_HD float hm_powf_idm(float b, float p) {
   const float fe = (float)e;
   y = hm_fma(-2.12194440e-4f, fe, y);
   y = hm_fma(-0.5f, z, y);
-  const float lg = hm_fma(0.693359375f, fe, x + y); /* log b (b > 0 normal) */
+  return hm_fma(0.693359375f, fe, x + y); /* log b (b > 0 normal) */
+}
+
+HWY_HD float hm_expf_idm(float lg, float p, float b) {
   const float t = p * lg;
   const float tc = hm_minf(hm_maxf(t, -87.0f), 88.0f);
   const float w = hm_fma(1.44269504088896341f, tc, 0.5f);
@@ -347,6 +353,8 @@ HWY_HD float hm_powf_idm(float b, float p) {
   res = b != b ? b : res;
   return b > 0.0f ? res : (b == 0.0f ? 0.0f : res);
 }
+
+HWY_HD float hm_powf_idm(float b, float p) { return hm_expf_idm(hm_logf_idm(b), p, b); }
 
 /* utils.wrap_to_pi: ((x + pi) % (2 pi)) - pi with Python's floored modulo.  The quotient is
  * taken with the reciprocal (a possible off-by-one next to a multiple of 2 pi is corrected

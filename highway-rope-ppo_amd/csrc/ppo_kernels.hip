@@ -2243,6 +2243,10 @@ struct OptArgs {
   int64_t o_w1, o_w2, o_wa1, o_wc1;
   int S, H, sb, hb;
   int skip;  // dev builds' pricing (HWY_PPO_SKIP, WRONG results): 1 no tile writes, 2 empty; 0
+  // ppo_adam_tiles: workgroups per weight matrix (W1, W2, Wa1, Wc1) and the small parameters'
+  // contiguous runs [b1], [b2], [ba1 wa2 ba2 log_std], [bc1 wc2 bc2] (flat offsets, prefix counts)
+  int nwg1, nwgh, nkg1;
+  int64_t run_off[4], run_pre[5];
 };
 
 // float index of B[k][n] in a tile image region with nblk blocks per 16 columns
@@ -2365,18 +2369,25 @@ __device__ __forceinline__ void adam_scalars(const OptArgs& o, float* red, float
   __syncthreads();
 }
 
+// torch.optim.Adam on one element after the clip: the raw gradient and the old state in, the new
+// moments and parameter out
+__device__ __forceinline__ void adam_math(const OptArgs& o, float g_raw, float& mm, float& vv,
+                                          float& p, const float* sh) {
+  const float coef = sh[0], step_size = sh[1], bc2_sqrt = sh[2];
+  const float g = g_raw * coef;
+  mm = mm + (1.0f - o.beta1) * (g - mm);  // exp_avg.lerp_(grad, 1 - beta1)
+  vv = vv * o.beta2 + (1.0f - o.beta2) * g * g;
+  const float denom = sqrtf(vv) / bc2_sqrt + o.eps;
+  p = p - step_size * (mm / denom);
+}
+
 // one element of torch.optim.Adam after the clip (parameter i, its raw gradient and old state)
 __device__ __forceinline__ void adam_elem(const OptArgs& o, int64_t i, float g_raw, float m_old,
                                           float v_old, float p_old, const float* sh) {
-  const float coef = sh[0], step_size = sh[1], bc2_sqrt = sh[2];
-  const float g = g_raw * coef;
-  float mm = m_old, vv = v_old;
-  mm = mm + (1.0f - o.beta1) * (g - mm);  // exp_avg.lerp_(grad, 1 - beta1)
-  vv = vv * o.beta2 + (1.0f - o.beta2) * g * g;
+  float mm = m_old, vv = v_old, pn = p_old;
+  adam_math(o, g_raw, mm, vv, pn, sh);
   o.m[i] = mm;
   o.v[i] = vv;
-  const float denom = sqrtf(vv) / bc2_sqrt + o.eps;
-  const float pn = p_old - step_size * (mm / denom);
   o.params[i] = pn;
   if (o.tiles) write_tiles(o, i, pn);
 }
@@ -2403,6 +2414,106 @@ __global__ void __launch_bounds__(256) ppo_adam(OptArgs o) {
     const int64_t i = ((int64_t)blockIdx.x * kAdamEPT + q) * 256 + threadIdx.x;
     if (i >= o.numel) break;
     adam_elem(o, i, g_raw[q], m_old[q], v_old[q], p_old[q], sh);
+  }
+}
+
+// ppo_adam over the fused path's weight tile image, tile-major: a weight workgroup takes 16 rows x
+// 64 columns of one of W1, W2, Wa1, Wc1 (wave w: the 16 x 16 block of columns 16w..16w+15; lane
+// l: row l & 15, columns 4 (l >> 4) .. + 3 as one float4), so each wave rewrites whole 1-KB image
+// blocks: the forward block (B = W^T) straight from its float4s (lane-linear), the backward block
+// (B = W) after a 4 x 4 transpose through LDS.  The small parameters (biases, heads, log_std)
+// follow in flat workgroups of 1,024.  Same Adam arithmetic per element as ppo_adam, so the same
+// bits; ppo_adam's one-element mapping scatters 4-byte image writes over 16 blocks per wave.
+__global__ void __launch_bounds__(256) ppo_adam_tiles(OptArgs o) {
+  __shared__ float red[4];
+  __shared__ float sh[3];
+  __shared__ __attribute__((aligned(16))) f32x4 tr[4][64];  // per wave: its block, [row][col]
+  const float first = (int)threadIdx.x < o.nred ? o.norm_part[threadIdx.x] : 0.0f;
+  const int step = o.counters[0];
+  const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
+  const int H = o.H;
+  if ((int)blockIdx.x < o.nwg1 + 3 * o.nwgh) {
+    int b = blockIdx.x, q, kg;
+    if (b < o.nwg1) {
+      q = 0, kg = o.nkg1;
+    } else {
+      b -= o.nwg1;
+      q = 1 + b / o.nwgh, b -= (q - 1) * o.nwgh, kg = H / 64;
+    }
+    const int n0 = 16 * (b / kg), k0 = 64 * (b % kg) + 16 * wv;  // this wave's block
+    const int K = q == 0 ? o.S : H;
+    const int64_t off = q == 0 ? o.o_w1 : (q == 1 ? o.o_w2 : (q == 2 ? o.o_wa1 : o.o_wc1));
+    const int nn = lane & 15, kq = lane >> 4;
+    const int k = k0 + 4 * kq;
+    const bool live = k < K;  // S % 4 == 0 (host check): a float4 is all live or all padding
+    const int64_t i = off + (int64_t)(n0 + nn) * K + k;
+    f32x4 g4 = {}, m4 = {}, v4 = {}, p4 = {};
+    if (live) {
+      g4 = *reinterpret_cast<const f32x4*>(o.grads + i);
+      m4 = *reinterpret_cast<const f32x4*>(o.m + i);
+      v4 = *reinterpret_cast<const f32x4*>(o.v + i);
+      p4 = *reinterpret_cast<const f32x4*>(o.params + i);
+    }
+    adam_scalars(o, red, sh, first, step);
+    if (o.skip & 2) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float mm = m4[j], vv = v4[j], pp = p4[j];
+      adam_math(o, g4[j], mm, vv, pp, sh);
+      m4[j] = mm, v4[j] = vv, p4[j] = pp;
+    }
+    if (live) {
+      *reinterpret_cast<f32x4*>(o.m + i) = m4;
+      *reinterpret_cast<f32x4*>(o.v + i) = v4;
+      *reinterpret_cast<f32x4*>(o.params + i) = p4;
+    } else {
+      p4 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};  // the image's zero padding past K
+    }
+    if ((o.skip & 1) || k0 >= K) return;  // a W1 block wholly past S: padding, already zero
+    const TileGeom T = tile_geom(o.S, H, o.sb, o.hb);
+    const int64_t fb = q == 0 ? T.f1 : (q == 1 ? T.f2 : (q == 2 ? T.fa : T.fc));
+    const int nblk = q == 0 ? o.sb : o.hb;
+    // forward image B[k][n] = W[n][k]: float 4 (16 kq + nn) + j of block (n0 / 16, k0 / 16)
+    *reinterpret_cast<f32x4*>(o.tiles + fb + ((int64_t)(n0 >> 4) * nblk + (k0 >> 4)) * 256 +
+                              4 * lane) = p4;
+    if (q == 0) return;  // W1 has no backward image (uniform per workgroup: no barrier below)
+    // backward image B[k'][n'] = W[k'][n'] (k' = row, n' = column): float
+    // 4 (16 (row >> 2) + col) + (row & 3) of block (k0 / 16, n0 / 16); lane 16 kq + 4 a + c takes
+    // rows 4a..4a+3 of column 4 kq + c from the block staged in LDS
+    tr[wv][nn * 4 + kq] = p4;
+    __syncthreads();
+    const float* blk = reinterpret_cast<const float*>(tr[wv]);
+    const int a = (lane >> 2) & 3, col = 4 * kq + (lane & 3);
+    const f32x4 o4 = {blk[(4 * a) * 16 + col], blk[(4 * a + 1) * 16 + col],
+                      blk[(4 * a + 2) * 16 + col], blk[(4 * a + 3) * 16 + col]};
+    const int64_t bb = q == 1 ? T.b2 : (q == 2 ? T.ba : T.bc);
+    *reinterpret_cast<f32x4*>(o.tiles + bb + ((int64_t)(k0 >> 4) * o.hb + (n0 >> 4)) * 256 +
+                              4 * (16 * a + col)) = o4;
+    return;
+  }
+  // the small parameters: four contiguous runs, 4 elements per thread 256 apart
+  const int64_t e0 = (int64_t)(blockIdx.x - o.nwg1 - 3 * o.nwgh) * 1024 + t;
+  float g_raw[4], m_old[4], v_old[4], p_old[4];
+  int64_t ii[4];
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq) {
+    const int64_t e = e0 + 256 * qq;
+    int r = 0;
+#pragma unroll
+    for (int z = 1; z < 4; ++z)
+      if (e >= o.run_pre[z]) r = z;
+    ii[qq] = e < o.run_pre[4] ? o.run_off[r] + (e - o.run_pre[r]) : -1;
+    const int64_t src = ii[qq] >= 0 ? ii[qq] : 0;
+    g_raw[qq] = o.grads[src], m_old[qq] = o.m[src], v_old[qq] = o.v[src], p_old[qq] = o.params[src];
+  }
+  adam_scalars(o, red, sh, first, step);
+  if (o.skip & 2) return;
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq) {
+    if (ii[qq] < 0) break;
+    float mm = m_old[qq], vv = v_old[qq], pp = p_old[qq];
+    adam_math(o, g_raw[qq], mm, vv, pp, sh);
+    o.m[ii[qq]] = mm, o.v[ii[qq]] = vv, o.params[ii[qq]] = pp;
   }
 }
 
@@ -2668,10 +2779,32 @@ int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream) {
     o.S = d.S, o.H = d.H, o.sb = w.sb, o.hb = w.hb;
   }
   o.skip = dev_knob_int("HWY_PPO_SKIP", 0) & 3;
+  // the tile-major kernel wherever its float4s are aligned: S % 4 == 0 and 16-byte aligned bases
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
+  if (w.fused && d.S % 4 == 0 && al16(o.params) && al16(o.grads) && al16(o.m) && al16(o.v) &&
+      dev_knob_int("HWY_ADAM_FLAT", 0) == 0) {
+    const int kb1 = (d.S + 15) / 16;  // W1's live 16-column blocks
+    o.nkg1 = (kb1 + 3) / 4;
+    o.nwg1 = (d.H / 16) * o.nkg1;
+    o.nwgh = (d.H / 16) * (d.H / 64);
+    const int64_t r0[4] = {L.off[P_B1], L.off[P_B2], L.off[P_BA1], L.off[P_BC1]};
+    const int64_t r1[4] = {L.off[P_W2], L.off[P_WA1], L.off[P_WC1], L.numel};
+    o.run_pre[0] = 0;
+    for (int z = 0; z < 4; ++z) {
+      o.run_off[z] = r0[z];
+      o.run_pre[z + 1] = o.run_pre[z] + (r1[z] - r0[z]);
+    }
+    const int nsmall = (int)((o.run_pre[4] + 1023) / 1024);
+    hipLaunchKernelGGL(ppo_adam_tiles, dim3(o.nwg1 + 3 * o.nwgh + nsmall), dim3(256), 0, s, o);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   const int nadam = (int)((L.numel + 256 * kAdamEPT - 1) / (256 * kAdamEPT));
   hipLaunchKernelGGL(ppo_adam, dim3(nadam), dim3(256), 0, s, o);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+// an empty workgroup: hwy_ppo_time_kernels' launch floor (a graph of dependent empty launches)
+__global__ void __launch_bounds__(64) ppo_nop() {}
 
 int hwy_ppo_time_kernels(const hwy_ppo_args* a, void* stream, int reps, float* us) {
   if (!a || !us || reps < 1 || a->grads_modified || !a->counters) return -1;
@@ -2679,7 +2812,8 @@ int hwy_ppo_time_kernels(const hwy_ppo_args* a, void* stream, int reps, float* u
   // Each kernel as its own HIP graph of `reps` back-to-back launches on a private stream,
   // replayed once to warm up and once between two events: the average launch of a kernel in the
   // same position it has in the epoch graph (graph-issued, dependent on its predecessor), without
-  // host launch costs.  The caller's Adam step count is restored afterwards; the metrics row
+  // host launch costs; us[4]: the same for an empty one-workgroup kernel, the per-launch floor
+  // (dispatch and completion of a dependent launch) that a kernel-trace duration leaves out.  The caller's Adam step count is restored afterwards; the metrics row
   // index is reset before each replay so ppo_wgrad always writes metrics row 0.
   if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return -2;
   int32_t saved[2];
@@ -2691,7 +2825,7 @@ int hwy_ppo_time_kernels(const hwy_ppo_args* a, void* stream, int reps, float* u
       hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)
     rc = -2;
   const int32_t one = 1;
-  for (int k = 0; k < 4 && rc == 0; ++k) {
+  for (int k = 0; k < 5 && rc == 0; ++k) {
     hipGraph_t g = nullptr;
     hipGraphExec_t x = nullptr;
     if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) {
@@ -2699,10 +2833,14 @@ int hwy_ppo_time_kernels(const hwy_ppo_args* a, void* stream, int reps, float* u
       break;
     }
     for (int i = 0; i < reps; ++i) {
-      if (k < 3)
+      if (k < 3) {
         rc |= forward_backward_k(a, s, 1 << k);
-      else
+      } else if (k == 3) {
         rc |= hwy_ppo_optimizer(a, s);
+      } else {
+        hipLaunchKernelGGL(ppo_nop, dim3(1), dim3(64), 0, s);
+        rc |= hipGetLastError() == hipSuccess ? 0 : -2;
+      }
     }
     rc |= hipStreamEndCapture(s, &g) == hipSuccess ? 0 : -2;
     if (rc == 0) rc = hipGraphInstantiate(&x, g, nullptr, nullptr, 0) == hipSuccess ? 0 : -2;

@@ -438,7 +438,8 @@ class FusedPPO:
     def time_kernels(self, reps: int = 16) -> Optional[dict]:
         """Average microseconds per launch of each kernel of the minibatch step (ppo_rows,
         ppo_wgrad, ppo_wsum, ppo_adam) on the last update's first minibatch, each as a HIP graph
-        of `reps` back-to-back launches (hwy_ppo_time_kernels).  A measurement aid for bench.py,
+        of `reps` back-to-back launches (hwy_ppo_time_kernels), and of an empty kernel
+        (`launch_floor`: the per-launch cost a kernel-trace duration leaves out).  A measurement aid for bench.py,
         run after its timed region: the Adam launches update the weights and moments as training
         steps do, and metrics row 0 is overwritten.  None before the first run()."""
         args = getattr(self, "_last_args", None)
@@ -447,12 +448,12 @@ class FusedPPO:
         a = PpoArgs.from_buffer_copy(args[0])
         a.grads_modified = 0  # this rank's own kernels only (no all-reduce between them)
         self.counters[1].zero_()
-        us = (ctypes.c_float * 4)()
+        us = (ctypes.c_float * 5)()
         check(self.L.hwy_ppo_time_kernels(ctypes.byref(a), stream_ptr(), max(1, int(reps)), us),
               "hwy_ppo_time_kernels")
         self.counters[1].zero_()
         self._tiles_version = self._param_versions()
-        return dict(zip(self.KERNELS, (float(u) for u in us)))
+        return dict(zip(self.KERNELS + ("launch_floor",), (float(u) for u in us)))
 
     def _epoch_event(self, start=None):
         if self.epoch_events is None:

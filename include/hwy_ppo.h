@@ -75,7 +75,8 @@ int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream);
 /* Measurement aid (bench.py's per-kernel roofline): each kernel of the minibatch step
  * (ppo_rows, ppo_wgrad, ppo_wsum, ppo_adam) captured as a HIP graph of `reps` back-to-back
  * launches on a private stream and replayed between two events; writes the average microseconds
- * per launch to us[4].  The Adam launches update params / moments / the tile image as training
+ * per launch to us[0..3], and to us[4] the same for an empty one-workgroup kernel (the launch
+ * floor a kernel-trace duration leaves out).  The Adam launches update params / moments / the tile image as training
  * steps do; the Adam step count is restored and the metrics row index left at 0.  Waits for
  * `stream` first; synchronous, not graph-capturable; fused path, grads_modified == 0.
  * -1 bad args, -2 HIP error. */
