@@ -746,11 +746,11 @@ struct LaneScan {
   uint64_t ahead, behind;  // candidate positions for the front / the rear of this vehicle
 };
 
+// xp: x of the vehicle at position `lane` (shf(v.x, o.ord), when the caller has it)
 __device__ __forceinline__ LaneScan lane_scan(int lane, const Veh& v, uint64_t pres,
-                                              const RoadOrder& o) {
+                                              const RoadOrder& o, float xp) {
   LaneScan L;
   const int npres = __popcll(pres);
-  const float xp = shf(v.x, o.ord);
   L.yp = shf(v.y, o.ord);
   L.okp = lane < npres && -LANE_VEH_LEN <= xp && xp < ROAD_LENGTH + LANE_VEH_LEN;
   const float xprev = shr1f(xp);
@@ -769,9 +769,9 @@ __device__ __forceinline__ uint64_t on_lane_mask(const LaneScan& L, int c) {
 // Also returns qf[s], the road-order position of front s (this vehicle's own position when
 // there is none), for gathers from position-space copies one bpermute level earlier.
 __device__ __forceinline__ void neighbours_ordered(const hwy_config& C, int lane, const Veh& v,
-                                                   uint64_t pres, const RoadOrder& o, int fi[3],
-                                                   int ri[3], int qfp[3]) {
-  const LaneScan L = lane_scan(lane, v, pres, o);
+                                                   uint64_t pres, const RoadOrder& o, float xq,
+                                                   int fi[3], int ri[3], int qfp[3]) {
+  const LaneScan L = lane_scan(lane, v, pres, o, xq);
   uint64_t m[3] = {0ull, 0ull, 0ull};
   for (int c = 0; c < C.lanes_count; ++c) {
     const uint64_t mc = on_lane_mask(L, c);
@@ -794,7 +794,7 @@ __device__ __forceinline__ void neighbours_ordered(const hwy_config& C, int lane
 // the front vehicle on an arbitrary lane c of each vehicle (same rule as neighbours_ordered)
 __device__ __forceinline__ int front_on_lane(const hwy_config& C, int lane, const Veh& v,
                                              uint64_t pres, const RoadOrder& o, int c_own) {
-  const LaneScan L = lane_scan(lane, v, pres, o);
+  const LaneScan L = lane_scan(lane, v, pres, o, shf(v.x, o.ord));
   uint64_t m = 0ull;
   for (int c = 0; c < C.lanes_count; ++c) {
     const uint64_t mc = on_lane_mask(L, c);
@@ -840,7 +840,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   const float vvx = v.spd * ch, vvy = v.spd * sh;
   const float xq = shf(v.x, ro.ord), vxq = shf(vvx, ro.ord), vyq = shf(vvy, ro.ord);
   int qfp[3];
-  neighbours_ordered(C, lane, v, pres, ro, fi, ri, qfp);
+  neighbours_ordered(C, lane, v, pres, ro, xq, fi, ri, qfp);
   SEC(sp, 1);
 
   // gathers (all lanes active); a missing front reads this vehicle's own values (unused)

@@ -62,7 +62,4 @@ def test_bench_two_ranks_one_line():
     assert all(pk[k]["us"] > 0 for k in ("ppo_rows", "ppo_wgrad", "ppo_wsum", "ppo_adam"))
     # the empty kernel's graph launch is the floor every kernel's launch pays
     assert 0 < pk["launch_floor_us"] < min(pk[k]["us"] for k in ("ppo_rows", "ppo_wsum"))
-    assert all(pk[k]["kernel_us"] == round(pk[k]["us"] - pk["launch_floor_us"], 2)
-               or abs(pk[k]["kernel_us"] - (pk[k]["us"] - pk["launch_floor_us"])) < 0.02
-               for k in ("ppo_rows", "ppo_wgrad", "ppo_wsum", "ppo_adam"))
     assert roof["flops_required_per_launch"] < roof["flops_per_launch"]
