@@ -436,6 +436,39 @@ def test_fused_optimizer_matches_torch_adam_on_identical_grads():
     assert torch.equal(F.grads, g_adam)
 
 
+def _tile_image_floats(S, H):
+    """TileGeom.total (csrc/ppo_kernels.hip tile_geom / rows_blocks): W1's forward image and six
+    H x H images, in 1-KB blocks, K zero-padded to whole ring groups."""
+    qh = H // 64
+    nw = 8 if qh % 2 == 0 else 4
+    d = 4 if H // nw // 16 <= 4 else 2
+    hb = -(-(H // 16) // d) * d
+    sb = -(-(-(-S // 16)) // d) * d
+    g = H // 16
+    return g * sb * 256 + 6 * g * hb * 256
+
+
+@pytest.mark.parametrize("S,H", [(60, 256), (200, 320), (136, 512), (120, 192), (60, 64)])
+def test_adam_rewrites_tile_image_as_a_rebuild(S, H):
+    """ppo_adam_tiles rewrites the weight tile image block by block (forward blocks lane-linear,
+    backward blocks through an LDS transpose, W1 blocks wholly past S left alone): after the
+    update's Adam steps the image equals hwy_ppo_sync_params' rebuild from the new params, bit
+    for bit, zero padding included.  (200, 320): a two-deep ring, so W1's 13 live blocks sit in
+    a 14-block image while the Adam workgroup spans 16."""
+    a, b = _agents(S, H)
+    n, nmb = 512, 2
+    s, z, lp, adv, ret, perm = _data(n, S, a)
+    F = FusedPPO(b, n // nmb, nmb, use_graphs=False)
+    F.run(s, z, lp, adv.clone(), ret.clone(), perm.clone())
+    torch.cuda.synchronize()
+    nb = _tile_image_floats(S, H) * 4
+    assert F._tile_off is not None and F._tile_off + nb <= F.workspace.numel()
+    img = F.workspace[F._tile_off:F._tile_off + nb].clone()
+    F.sync_params(F._args(s, z, lp, adv, ret, perm.data_ptr()))
+    torch.cuda.synchronize()
+    assert torch.equal(F.workspace[F._tile_off:F._tile_off + nb], img)
+
+
 def test_fused_state_roundtrip_to_torch_optimizer(tmp_path):
     S, H = 60, 64
     a, b = _agents(S, H)
