@@ -260,7 +260,7 @@ int hwy_gae(const float* rewards, const uint8_t* dones, const float* values,
 }
 
 int hwy_math_selftest(int op, const float* in, const float* in2, float* out, int n, void* stream) {
-  if (op < 0 || op > 15 || n < 0) return fail(HWY_EINVAL, "bad selftest op %d", op);
+  if (op < 0 || op > 16 || n < 0) return fail(HWY_EINVAL, "bad selftest op %d", op);
   if (hwy_launch_math(op, in, in2, out, n, (hipStream_t)stream))
     return hip_fail(hipGetLastError(), "hwy_math_kernel");
   return HWY_OK;

@@ -202,7 +202,8 @@ __device__ __forceinline__ bool on_lane_m(float x, float y, int c, float margin)
          x < ROAD_LENGTH + LANE_VEH_LEN;
 }
 
-__device__ __forceinline__ int closest_lane(float y, int lanes) {
+// the loop form: the first lane of least |lateral offset| (upstream's argmin over the lanes)
+__device__ __forceinline__ int closest_lane_scan(float y, int lanes) {
   int best = 0;
   float bd = hm_absf(lane_lat(y, 0));
   for (int c = 1; c < lanes; ++c) {
@@ -213,6 +214,19 @@ __device__ __forceinline__ int closest_lane(float y, int lanes) {
     }
   }
   return best;
+}
+
+// closest_lane_scan's answer from two candidates: for |y| < 2^20 (lane offsets exact to 1/8) the
+// first least offset is c0 = floor(y / 4) clamped to the lanes, or c0 + 1 if its offset is
+// strictly smaller.  Below c0 the offsets are >= 4 > |offset(c0)| (y - 4 c0 is exact, Sterbenz),
+// above c0 + 1 likewise; outside the road the offsets are strictly monotone in c.  Any other y
+// (and NaN) takes the scan.
+__device__ __forceinline__ int closest_lane(float y, int lanes) {
+  if (!(hm_absf(y) < 1048576.0f)) return closest_lane_scan(y, lanes);
+  const float q = hm_floorf(y * (1.0f / LANE_WIDTH));
+  const int c0 = q >= (float)(lanes - 1) ? lanes - 1 : (q > 0.0f ? (int)q : 0);
+  const bool up = c0 + 1 < lanes && hm_absf(lane_lat(y, c0 + 1)) < hm_absf(lane_lat(y, c0));
+  return up ? c0 + 1 : c0;
 }
 
 // IDMVehicle.desired_gap(ego=a, front=b), from the velocity vectors (speed * (cos h, sin h),
@@ -1352,6 +1366,7 @@ __global__ void hwy_math_kernel(int op, const float* in, const float* in2, float
     case 13: { float s_; hm_sincosf(x, &s_, &r); } break;
     case 14: r = hm_tanf_sc(x); break;
     case 15: r = hm_powf_idm(x, y); break;
+    case 16: r = (float)closest_lane(x, (int)y); break;  // y: lanes_count
   }
   out[i] = r;
 }

@@ -993,6 +993,7 @@ int hwyo_math(int op, const float* in, const float* in2, float* out, int n) {
       case 13: { float s_; hm_sincosf(x, &s_, &r); } break;
       case 14: r = hm_tanf_sc(x); break;
       case 15: r = hm_powf_idm(x, y); break;
+      case 16: r = (float)closest_lane(x, (int)y); break; /* y: lanes_count (the scan) */
       default: return -1;
     }
     out[i] = r;

@@ -27,6 +27,15 @@ def _inputs(op, rng, n=200000):
         x = np.abs(rng.uniform(0, 4000, n))
     elif op == 15:  # the IDM pow: base >= 0 over every binary32 exponent
         x = (rng.uniform(1, 2, n) * np.exp2(rng.integers(-149, 128, n).astype(np.float64)))
+    elif op == 16:  # closest lane: the road, its lane-centre ties (4c + 2) and their neighbours,
+        # beyond the road, and |y| around the 2^20 switch to the scan
+        ties = np.arange(-8, 40, 2, dtype=np.float32)
+        near = np.concatenate([np.nextafter(ties, np.float32(np.inf)),
+                               np.nextafter(ties, np.float32(-np.inf))])
+        big = np.array([2.0 ** 20, -2.0 ** 20, np.nextafter(np.float32(2.0 ** 20), np.float32(0)),
+                        1e9, -1e9, 3e7, 123456.7], np.float32)
+        x = np.concatenate([rng.uniform(-20, 40, n - 2 * ties.size - big.size), ties, near[:ties.size],
+                            near[ties.size:], big])
     else:
         x = rng.normal(0, 100, n)
     y = None
@@ -34,6 +43,8 @@ def _inputs(op, rng, n=200000):
         y = rng.uniform(-4.5, 4.5, n)
     if op == 15:
         y = rng.uniform(3.5, 4.5, n)
+    if op == 16:
+        y = rng.integers(1, 7, x.size).astype(np.float64)
     if op == 10:
         y = rng.normal(0, 10, n)
     # IEEE special values and range edges ride along with every op
@@ -41,13 +52,13 @@ def _inputs(op, rng, n=200000):
                    1.0, -1.0, 0.5, np.pi / 2, np.pi, 2 * np.pi], np.float32)
     x = np.concatenate([x, sp])
     if y is not None:
-        y = np.concatenate([y, np.full(sp.size, {10: 3.0, 15: 4.0}.get(op, 2.0))])
+        y = np.concatenate([y, np.full(sp.size, {10: 3.0, 15: 4.0, 16: 4.0}.get(op, 2.0))])
     if op == 15:  # the IDM base is >= 0 (or NaN)
         x = np.where(np.signbit(x), -x, x)
     return x.astype(np.float32), None if y is None else y.astype(np.float32)
 
 
-@pytest.mark.parametrize("op", list(range(16)))
+@pytest.mark.parametrize("op", list(range(17)))
 def test_math_library_bit_exact(op):
     rng = np.random.default_rng(op)
     x, y = _inputs(op, rng)
