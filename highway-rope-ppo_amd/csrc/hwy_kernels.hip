@@ -109,7 +109,9 @@ __device__ __forceinline__ float wave_max_f(float v) {
       __builtin_amdgcn_update_dpp(b, b, 0x143, 0xc, 0xf, false))));
   return __int_as_float(__builtin_amdgcn_readlane(b, 63));
 }
-__device__ __forceinline__ uint64_t ballot(bool p) { return (uint64_t)__ballot(p); }
+// the lane mask of p straight from the compare (HIP's __ballot(int) re-materialises p as an
+// int and compares it again: two VALU per ballot)
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ bool wave_any(bool p) { return ballot(p) != 0ull; }
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -299,16 +301,19 @@ __device__ __forceinline__ float interval_distance(float min_a, float max_a, flo
   return min_a < min_b ? min_b - max_a : min_a - max_b;
 }
 
-// `active`: this lane holds a pair.  The wave stops once every active lane has broken out
+// `activem`: the lanes holding a pair.  The wave stops once every active lane has broken out
 // (nothing changes for a lane after its break), which after a's own two normals is the usual
-// case: cars in adjacent lanes separate on v_a, cars in one lane on u_a.
-__device__ __forceinline__ void sat_collide(bool active, float xa, float ya, float ca, float sa,
+// case: cars in adjacent lanes separate on v_a, cars in one lane on u_a.  Each edge runs on every
+// lane: a lane already out has inter = will = false, which the edge's updates keep (the same
+// values upstream's break leaves); the break test reads wave masks kept from the compares.
+__device__ __forceinline__ void sat_collide(uint64_t activem, float xa, float ya, float ca, float sa,
                                             float dax, float day, float xb, float yb, float cb,
                                             float sb, float dbx, float dby, bool* inter_out,
                                             bool* will_out, float* tx, float* ty) {
   const float cdx = xa - xb, cdy = ya - yb;
   const float ddx = dax - dbx, ddy = day - dby;
   bool inter = true, will = true;
+  uint64_t interm = activem, willm = activem;  // ballot(active && inter), ballot(active && will)
   float min_distance = __builtin_huge_valf(), axx = 0.0f, axy = 0.0f;
   float pa0[2], pa1[2], pb0[2], pb1[2], vpk[2], cdk[2], nxk[2], nyk[2];
 #pragma unroll
@@ -329,21 +334,25 @@ __device__ __forceinline__ void sat_collide(bool active, float xa, float ya, flo
       min_a = -pa1[k], max_a = -pa0[k], min_b = -pb1[k], max_b = -pb0[k];
       vp = -vpk[k], cd = -cdk[k], sx = -nxk[k], sy = -nyk[k];
     }
-    if (inter || will) {  // upstream breaks out once both are false
-      if (interval_distance(min_a, max_a, min_b, max_b) > 0.0f) inter = false;
+    {  // upstream breaks out once both are false (a lane past that keeps both false here)
+      const bool s0 = interval_distance(min_a, max_a, min_b, max_b) > 0.0f;
+      inter = inter && !s0;
       if (vp < 0.0f)
         min_a = min_a + vp;
       else
         max_a = max_a + vp;
       const float distance = interval_distance(min_a, max_a, min_b, max_b);
-      if (distance > 0.0f) will = false;
+      const bool s1 = distance > 0.0f;
+      will = will && !s1;
+      interm &= ~ballot(s0);
+      willm &= ~ballot(s1);
       if ((inter || will) && hm_absf(distance) < min_distance) {
         min_distance = hm_absf(distance);
         axx = cd > 0.0f ? sx : -sx;
         axy = cd > 0.0f ? sy : -sy;
       }
     }
-    if ((e & 1) && e < 7 && !wave_any(active && (inter || will))) break;
+    if ((e & 1) && e < 7 && !(interm | willm)) break;
   }
   *inter_out = inter;
   *will_out = will;
@@ -693,7 +702,7 @@ __device__ void road_order(int lane, const Veh& v, uint64_t pres, RoadOrder& o) 
   if (o.valid) {
     uint64_t kp = shf64(key, o.ord);
     uint64_t kn = shl1_64(kp);  // the next position's key (DPP)
-    sorted = !wave_any(lane < WAVE - 1 && !(kp < kn));
+    sorted = (~ballot(kp < kn) & (~0ull >> 1)) == 0ull;  // every position but the last ascends
     // a few overtakes since the last frame: odd-even transposition rounds on (key, vehicle)
     // in position space usually restore the order without a full re-rank; the partner is
     // lane ^ 1 in the even phase and lane + 1 / lane - 1 (odd / even lane) in the odd one
@@ -720,7 +729,7 @@ __device__ void road_order(int lane, const Veh& v, uint64_t pres, RoadOrder& o) 
         ordp = swap ? po : ordp;
       }
       kn = shl1_64(kp);
-      sorted = !wave_any(lane < WAVE - 1 && !(kp < kn));
+      sorted = (~ballot(kp < kn) & (~0ull >> 1)) == 0ull;
     }
     if (sorted) {
       o.ord = ordp;
@@ -757,6 +766,7 @@ __device__ void road_order(int lane, const Veh& v, uint64_t pres, RoadOrder& o) 
 struct LaneScan {
   float yp;      // y of the vehicle at position `lane`
   bool okp;      // that vehicle is present and inside the road's x range
+  uint64_t okm;  // ballot(okp)
   uint64_t ahead, behind;  // candidate positions for the front / the rear of this vehicle
 };
 
@@ -767,8 +777,9 @@ __device__ __forceinline__ LaneScan lane_scan(int lane, const Veh& v, uint64_t p
   const int npres = __popcll(pres);
   L.yp = shf(v.y, o.ord);
   L.okp = lane < npres && -LANE_VEH_LEN <= xp && xp < ROAD_LENGTH + LANE_VEH_LEN;
+  L.okm = ballot(lane < npres) & ballot(-LANE_VEH_LEN <= xp) & ballot(xp < ROAD_LENGTH + LANE_VEH_LEN);
   const float xprev = shr1f(xp);
-  const uint64_t starts = ballot(lane == 0 || !(xprev == xp));  // x-group starts (bit 0 set)
+  const uint64_t starts = ballot(xprev != xp) | 1ull;  // x-group starts (bit 0 set)
   const int g = 63 - __builtin_clzll(starts & ((2ull << o.rk) - 1ull));  // rk = 63: all ones
   const bool selfok = v.x == v.x;
   L.ahead = selfok ? (~0ull << g) & ~(1ull << o.rk) : 0ull;
@@ -777,7 +788,8 @@ __device__ __forceinline__ LaneScan lane_scan(int lane, const Veh& v, uint64_t p
 }
 
 __device__ __forceinline__ uint64_t on_lane_mask(const LaneScan& L, int c) {
-  return ballot(L.okp && hm_absf(lane_lat(L.yp, c)) <= LANE_WIDTH / 2.0f + 1.0f);
+  // (the compare's own mask, then a scalar AND: a ballot of p && q costs two VALU more)
+  return ballot(hm_absf(lane_lat(L.yp, c)) <= LANE_WIDTH / 2.0f + 1.0f) & L.okm;
 }
 
 // Also returns qf[s], the road-order position of front s (this vehicle's own position when
@@ -787,11 +799,31 @@ __device__ __forceinline__ void neighbours_ordered(const hwy_config& C, int lane
                                                    int fi[3], int ri[3], int qfp[3]) {
   const LaneScan L = lane_scan(lane, v, pres, o, xq);
   uint64_t m[3] = {0ull, 0ull, 0ull};
-  for (int c = 0; c < C.lanes_count; ++c) {
-    const uint64_t mc = on_lane_mask(L, c);
+  if (C.lanes_count <= WAVE - 2) {
+    // lane c's position mask (wave-uniform) goes to lane c + 1 of a VGPR pair (lanes 0 and
+    // lanes_count + 1 .. 63 hold no lane: 0), and each vehicle reads its slots ln .. ln + 2
+    int tlo = 0, thi = 0;
+    for (int c = 0; c < C.lanes_count; ++c) {
+      const uint64_t mc = on_lane_mask(L, c);
+      const bool mine = lane == c + 1;
+      tlo = mine ? (int)(uint32_t)mc : tlo;
+      thi = mine ? (int)(uint32_t)(mc >> 32) : thi;
+    }
 #pragma unroll
-    for (int s = 0; s < 3; ++s)
-      if (c == v.ln - 1 + s) m[s] = mc;
+    for (int s = 0; s < 3; ++s) {
+      const int src = v.ln + s;  // slot of lane ln - 1 + s
+      const bool in = src >= 0 && src < WAVE;
+      const int q = in ? src : 0;
+      const uint64_t mq = ((uint64_t)(uint32_t)shi(thi, q) << 32) | (uint32_t)shi(tlo, q);
+      m[s] = in ? mq : 0ull;
+    }
+  } else {
+    for (int c = 0; c < C.lanes_count; ++c) {
+      const uint64_t mc = on_lane_mask(L, c);
+#pragma unroll
+      for (int s = 0; s < 3; ++s)
+        if (c == v.ln - 1 + s) m[s] = mc;
+    }
   }
 #pragma unroll
   for (int s = 0; s < 3; ++s) {
@@ -829,12 +861,12 @@ struct CollLds {
 
 // ------------------------------------------------------------------------- one frame
 // Road.act() then Road.step(dt) for the env of this wave (lane = vehicle).
+// pres: ballot(v.present), fixed for the step (presence changes only at a reset)
 __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, float tan_ego, RoadOrder& ro,
-                           float& cos_h, float& sin_h, CollLds& cl, SecProf& sp) {
+                           float& cos_h, float& sin_h, CollLds& cl, SecProf& sp, uint64_t pres) {
   const int lanes = C.lanes_count;
   const float limit = C.speed_limit;
   const float ch = cos_h, sh = sin_h;  // cos / sin of v.h (carried from the previous frame)
-  const uint64_t pres = ballot(v.present);
 
   // ---------------- Road.act: IDMVehicle.act for every non-crashed traffic car
   const bool actor = v.present && lane >= 1 && !v.crashed;
@@ -937,11 +969,13 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   // abort an ongoing lane change if another car targets the same lane within its desired gap,
   // in road order (lower indices already final, higher ones at their frame-start target)
   int tl_cur = ntl;
-  uint64_t cm = (kSkip & 8) ? 0ull : ballot(actor && mid);
+  // (wave masks from the compares' own masks: a ballot of a compound bool costs two VALU)
+  const uint64_t actm = pres & ~1ull & ~ballot(v.crashed);  // ballot(actor)
+  uint64_t cm = (kSkip & 8) ? 0ull : actm & ballot(v.ln != v.tl);  // actor && mid
   // a lane can trigger an abort only while its visible target is not its own lane (vis == tj
   // and ln != tj), under either visibility; aborts only ever clear that, so this superset holds
   // for the whole loop
-  const bool can = v.present && lane != 0 && (tl_cur != v.ln || tl_old != v.ln);
+  const uint64_t canm = pres & ~1ull & (ballot(tl_cur != v.ln) | ballot(tl_old != v.ln));
   while (cm) {
     const int j = __builtin_ctzll(cm);
     cm &= cm - 1ull;
@@ -949,13 +983,13 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
     const int vis = (lane < j) ? tl_cur : tl_old;
     // the target-lane part of upstream's test first: most vehicles find no other car targeting
     // their lane, and then the gap test (four broadcasts and a desired_gap) is skipped
-    const bool cheap = can && lane != j && v.ln != tj && vis == tj;
-    if (!wave_any(cheap)) continue;
+    const uint64_t cheapm = canm & ~(1ull << j) & ballot(v.ln != tj) & ballot(vis == tj);
+    if (!cheapm) continue;
     const float xj = rdlf(v.x, j), vj = rdlf(v.spd, j), cj = rdlf(ch, j), sj = rdlf(sh, j);
     const float d = v.x - xj;
     const float d_star = desired_gap_v(vj, cj, sj, vj * cj, vj * sj, vvx, vvy);
-    const bool cond = cheap && (0.0f < d) && (d < d_star);
-    if (wave_any(cond) && lane == j) tl_cur = v.ln;
+    const uint64_t condm = cheapm & ballot(0.0f < d) & ballot(d < d_star);
+    if (condm && lane == j) tl_cur = v.ln;
   }
   v.tl = tl_cur;
 
@@ -966,7 +1000,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   if (v.tl == v.ln - 1) ft = fi[0];
   if (v.tl == v.ln + 1) ft = fi[2];
   const bool extra = need_t && !(v.tl == v.ln - 1 || v.tl == v.ln + 1);
-  if (wave_any(extra)) {  // target lane not adjacent (rare): its own lane mask
+  if (actm & ballot(v.ln != v.tl) & ~ballot(v.tl == v.ln - 1) & ~ballot(v.tl == v.ln + 1)) {  // target lane not adjacent (rare): its own lane mask
     const int fx = front_on_lane(C, lane, v, pres, ro, v.tl);
     if (extra) ft = fx;
   }
@@ -1032,11 +1066,13 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   // that bound, taken here with the wave's largest speed (and widened past any rounding; a
   // non-finite speed or position disables the filter).
   float vabs = v.present ? hm_absf(v.spd) : 0.0f;
-  bool nonfinite = v.present && !(hm_absf(v.x) <= 3.0e38f && hm_absf(v.y) <= 3.0e38f &&
-                                  hm_absf(v.spd) <= 3.0e38f);
+  // any present vehicle with a non-finite x, y or speed (the compares' own masks)
+  const uint64_t nonfinite = pres & (ballot(!(hm_absf(v.x) <= 3.0e38f)) |
+                                     ballot(!(hm_absf(v.y) <= 3.0e38f)) |
+                                     ballot(!(hm_absf(v.spd) <= 3.0e38f)));
   vabs = wave_max_f(vabs);
-  const float xbound = wave_any(nonfinite) ? __builtin_huge_valf()
-                                           : (VEH_DIAGONAL + vabs * dt) * 1.001f + 1.0e-3f;
+  const float xbound = nonfinite ? __builtin_huge_valf()
+                                 : (VEH_DIAGONAL + vabs * dt) * 1.001f + 1.0e-3f;
   // x-sorted road order, in position space (lane = position p, holding vehicle ord[p]): the
   // candidates are the pairs (p, p+o) whose |dx| is within the bound.  x is monotone along the
   // order, so the run from p upwards is contiguous and every pair is found once, from its lower
@@ -1047,13 +1083,21 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
     const int npres = __popcll(pres);
     const float xs = shf(v.x, ro.ord);  // x at position `lane`
     float xu = xs;
+    // the loop runs on the wave mask U = ballot(up), kept from the compares' own masks (a
+    // ballot of a compound or loop-carried bool re-materialises it: two VALU), and counts each
+    // position's run; its candidates are o = 1 .. run
     bool up = lane < npres;
-    if (kSkip & 4) up = false;
-    for (int o = 1; wave_any(up); ++o) {
+    uint64_t U = (kSkip & 4) ? 0ull : ballot(lane < npres);
+    int run = 0;
+    for (int o = 1; U; ++o) {
       xu = __int_as_float(shl1i(__float_as_int(xu)));  // x at position lane + o
-      up = up && lane + o < npres && !(hm_absf(xu - xs) > xbound);
-      if (up) om |= 1ull << o;
+      const bool inr = lane < npres - o;
+      const bool far = hm_absf(xu - xs) > xbound;
+      up = up && inr && !far;
+      U &= ballot(inr) & ~ballot(far);
+      run += up ? 1 : 0;
     }
+    om = (2ull << run) - 2ull;  // bits 1 .. run (run <= 63)
   }
   SEC(sp, 10);
   // Each candidate pair once, spread over the lanes: position p lists its pairs (as vehicle
@@ -1061,7 +1105,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   // Per vehicle, upstream keeps the impact of its highest-index partner (the last
   // handle_collisions call that writes it) and ORs the crash flag; the translation therefore
   // goes through a 64-bit LDS max keyed by (partner + 1) in the high word.
-  const int cnt = __popcll(om);
+  const int cnt = __popcll(om);  // = run
   int off = wave_incl_scan(cnt);
   const int total = rdli(off, WAVE - 1);
   off -= cnt;
@@ -1088,9 +1132,23 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
                 vb = shf(v.spd, b);
     // exact pre-check (are_polygons_intersecting is only called inside it), then the SAT test
     const float dx = xb - xa, dy = yb - ya;
-    bool pass = has && !(__builtin_sqrtf(hm_fma(dx, dx, dy * dy)) >
-                         (VEH_DIAGONAL + VEH_DIAGONAL) / 2.0f + va * dt);
-    if (!wave_any(pass)) continue;
+    // upstream's sqrt(dx^2 + dy^2) > B, decided from the squares where they are 2^-19 apart (a
+    // margin far above the roundings of B^2 and of the thresholds: the correctly rounded root
+    // lies on the same side of B); a lane near the boundary, with B outside [1e-10, 2^60) or a
+    // non-finite square, takes the root itself
+    const float q2 = hm_fma(dx, dx, dy * dy);
+    const float bb = (VEH_DIAGONAL + VEH_DIAGONAL) / 2.0f + va * dt;
+    const float b2 = bb * bb;
+    const uint64_t bokm = ballot(bb >= 1.0e-10f) & ballot(bb < 0x1p60f);
+    const bool gt = q2 > b2 * (1.0f + 0x1p-19f), lt = q2 < b2 * (1.0f - 0x1p-19f);
+    bool far = gt;
+    if (~(bokm & (ballot(gt) | ballot(lt)))) {  // some lane undecided (rare): its root
+      const bool sure = (bb >= 1.0e-10f && bb < 0x1p60f) && (gt || lt);
+      far = sure ? gt : __builtin_sqrtf(q2) > bb;
+    }
+    bool pass = has && !far;
+    uint64_t passm = ballot(lane < total - base) & ~ballot(far);  // ballot(pass), compares' masks
+    if (!passm) continue;
     const float dax = (va * ca) * dt, day = (va * sa) * dt, dbx = (vb * cb) * dt, dby = (vb * sb) * dt;
     // a's v axis (the SAT's second edge normal) first: a pair separated on it both as it stands
     // and swept by the velocities ends with intersecting = will_intersect = false and no
@@ -1102,15 +1160,16 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
       rect_interval(xa, ya, ca, sa, -sa, ca, a0, a1);
       rect_interval(xb, yb, cb, sb, -sa, ca, b0, b1);
       const float vp = hm_fma(-sa, dax - dbx, ca * (day - dby));
-      const bool sep = interval_distance(a0, a1, b0, b1) > 0.0f &&
-                       interval_distance(vp < 0.0f ? a0 + vp : a0, vp < 0.0f ? a1 : a1 + vp, b0,
-                                         b1) > 0.0f;
-      pass = pass && !sep;
-      if (!wave_any(pass)) continue;
+      const bool sep0 = interval_distance(a0, a1, b0, b1) > 0.0f;
+      const bool sep1 = interval_distance(vp < 0.0f ? a0 + vp : a0, vp < 0.0f ? a1 : a1 + vp, b0,
+                                          b1) > 0.0f;
+      pass = pass && !(sep0 && sep1);
+      passm &= ~(ballot(sep0) & ballot(sep1));
+      if (!passm) continue;
     }
     bool inter, will;
     float tx, ty;
-    sat_collide(pass, xa, ya, ca, sa, dax, day, xb, yb, cb, sb, dbx, dby, &inter, &will, &tx, &ty);
+    sat_collide(passm, xa, ya, ca, sa, dax, day, xb, yb, cb, sb, dbx, dby, &inter, &will, &tx, &ty);
     if (pass && will) {
       atomicMax(&cl.imx[a], ((uint64_t)(b + 1) << 32) | hm_f2bits(tx / 2.0f));
       atomicMax(&cl.imy[a], ((uint64_t)(b + 1) << 32) | hm_f2bits(ty / 2.0f));
@@ -1184,7 +1243,8 @@ hwy_step_kernel(StepParams P) {
   ro.rk = lane < V ? order_pos : V + (WAVE - 1 - lane);
   ro.ord = __builtin_amdgcn_ds_permute(ro.rk << 2, lane);
   ro.valid = true;
-  road_order(lane, v, ballot(v.present), ro);
+  const uint64_t pres = ballot(v.present);
+  road_order(lane, v, pres, ro);
   float cos_h, sin_h;
   hm_sincosf(v.h, &sin_h, &cos_h);
   SEC(sp, 15);
@@ -1195,7 +1255,7 @@ hwy_step_kernel(StepParams P) {
   // the ego's steering changes only here and to 0 on a crash (handled in frame_wave)
   const float tan_ego = rdlf(lane == 0 ? hm_tanf_sc(v.asteer) : 0.0f, 0);
   for (int frame = 0; frame < frames; ++frame)
-    frame_wave(C, lane, v, dt, tan_ego, ro, cos_h, sin_h, lds_coll[w], sp);
+    frame_wave(C, lane, v, dt, tan_ego, ro, cos_h, sin_h, lds_coll[w], sp, pres);
   step += 1;
   SEC(sp, 11);
 
