@@ -1078,7 +1078,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   // order, so the run from p upwards is contiguous and every pair is found once, from its lower
   // position; x at p+o comes from a one-lane DPP shift per step (equal x sit together; a NaN x,
   // or any non-finite value, makes the bound infinite: every pair of present vehicles).
-  uint64_t om = 0ull;  // bit o: (p, p+o) is a candidate pair
+  int run = 0;  // the candidates of position p: (p, p + o) for o = 1 .. run
   {
     const int npres = __popcll(pres);
     const float xs = shf(v.x, ro.ord);  // x at position `lane`
@@ -1088,7 +1088,6 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
     // position's run; its candidates are o = 1 .. run
     bool up = lane < npres;
     uint64_t U = (kSkip & 4) ? 0ull : ballot(lane < npres);
-    int run = 0;
     for (int o = 1; U; ++o) {
       xu = __int_as_float(shl1i(__float_as_int(xu)));  // x at position lane + o
       const bool inr = lane < npres - o;
@@ -1097,7 +1096,6 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
       U &= ballot(inr) & ~ballot(far);
       run += up ? 1 : 0;
     }
-    om = (2ull << run) - 2ull;  // bits 1 .. run (run <= 63)
   }
   SEC(sp, 10);
   // Each candidate pair once, spread over the lanes: position p lists its pairs (as vehicle
@@ -1105,7 +1103,7 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   // Per vehicle, upstream keeps the impact of its highest-index partner (the last
   // handle_collisions call that writes it) and ORs the crash flag; the translation therefore
   // goes through a 64-bit LDS max keyed by (partner + 1) in the high word.
-  const int cnt = __popcll(om);  // = run
+  const int cnt = run;
   int off = wave_incl_scan(cnt);
   const int total = rdli(off, WAVE - 1);
   off -= cnt;
@@ -1114,9 +1112,8 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   cl.crash[lane] = 0;
   cl.pord[lane] = ro.ord;
   wave_lds_sync();
-  while (om) {
-    const int o = __builtin_ctzll(om);
-    om &= om - 1ull;
+#pragma unroll 1
+  for (int o = 1; o <= run; ++o) {
     const int q = cl.pord[lane + o];
     const int lo = ro.ord < q ? ro.ord : q, hi = ro.ord < q ? q : ro.ord;
     cl.plist[off++] = (uint16_t)((lo << 8) | hi);
