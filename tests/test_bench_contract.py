@@ -66,3 +66,26 @@ def test_metric_string_is_baselines():
 
     b = _bench()
     assert b.BASELINE_METRIC == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+
+
+def test_per_kernel_roofline_reproduces_from_the_cited_rocprof_file():
+    """The line's per-kernel roofline from the committed rocprofv3 summary of its workload
+    (bench.rocprof_per_kernel): the four kernels parse, and their summed
+    durations reproduce the committed default line's epoch-event step time within 2 %."""
+    import json
+    import os
+
+    import bench
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    line = json.loads(open(os.path.join(root, "profiles", "r5", "measure", "bench_c1.json"))
+                      .read().strip().splitlines()[-1])
+    roof = line["roofline"]
+    kf = bench.ppo_kernel_flops_per_sample(60, 256)
+    got = bench.rocprof_per_kernel((1, 4096, 32, 256), kf, roof["rows_per_launch"],
+                                   roof["avg_launch_us"])
+    assert got is not None and got["source"].endswith("kernel_stats_c1.txt")
+    assert all(got[k]["us"] > 0 for k in ("ppo_rows", "ppo_wgrad", "ppo_wsum", "ppo_adam"))
+    assert abs(got["sum_us"] / roof["avg_launch_us"] - 1.0) < 0.02
+    # no summary of an unmeasured workload
+    assert bench.rocprof_per_kernel((3, 8192, 128, 256), kf, 1, 1.0) is None
