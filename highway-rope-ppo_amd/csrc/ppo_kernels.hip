@@ -2607,6 +2607,8 @@ static int forward_backward_k(const hwy_ppo_args* a, void* stream, int mask) {
         case 1: hipLaunchKernelGGL((ppo_rows<1, 4, 16>), g1, b4, 0, s, r); break;
         case 2: hipLaunchKernelGGL((ppo_rows<2, 8, 16>), g1, b8, 0, s, r); break;
         case 3: hipLaunchKernelGGL((ppo_rows<3, 4, 16>), g1, b4, 0, s, r); break;
+        // (16 waves, one 16-column tile each, measured 73.2-73.6 vs 72.0-72.6 us per 4,096-row
+        // step, round 5; its head sums would also leave ppo_act_c's order)
         case 4: hipLaunchKernelGGL((ppo_rows<4, 8, 16>), g1, b8, 0, s, r); break;
         case 5: hipLaunchKernelGGL((ppo_rows<5, 4, 16>), g1, b4, 0, s, r); break;
         case 6: hipLaunchKernelGGL((ppo_rows<6, 8, 16>), g1, b8, 0, s, r); break;
