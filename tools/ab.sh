@@ -11,6 +11,9 @@
 #   MODE=act   VARS=... [ROWS="4096 16384 32768"]    ppo_act kernel-trace time (tools/probe_act.py)
 # TESTS=1 first runs the parity tests of the touched kernel on the product library and every
 # variant (tests/test_ppo_fused_gpu.py for ppo/act, tests/test_env_parity_gpu.py for step/pmc).
+# KNOBS="NAME=v ..." (MODE=ppo): also runs the dev build (VARS must hold its name, e.g. dev) once
+# per runtime knob setting (HWY_ADAM_FLAT=1, HWY_PPO_SKIP=1|2: timing-only pricing builds).
+# PROBE_KT=1 prints each kernel's time too (hwy_ppo_time_kernels).
 set -o pipefail
 R=$(pwd)
 H=$R/highway-rope-ppo_amd/hwy
@@ -37,6 +40,10 @@ ppo)
       for lib in $LIBS; do
         HWY_LIB=$H/$lib timeout -k 10 90 python -u tools/probe_ppo_time.py $Hd 10 $mb $S \
           | sed "s/^/$lib H=$Hd mb=$mb S=$S /" || exit 1
+      done
+      for kn in ${KNOBS:-}; do
+        env $kn HWY_LIB=$H/libhwy_${VARS%% *}.so timeout -k 10 90 python -u tools/probe_ppo_time.py \
+          $Hd 10 $mb $S | sed "s/^/${VARS%% *} $kn H=$Hd mb=$mb S=$S /" || exit 1
       done
     done
   done ;;
