@@ -1142,12 +1142,14 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
     const uint64_t bokm = ballot(bb >= 1.0e-10f) & ballot(bb < 0x1p60f);
     const bool gt = q2 > b2 * (1.0f + 0x1p-19f), lt = q2 < b2 * (1.0f - 0x1p-19f);
     bool far = gt;
-    if (~(bokm & (ballot(gt) | ballot(lt)))) {  // some lane undecided (rare): its root
+    uint64_t farm = ballot(gt);  // ballot(far), from the compare's own mask on the usual path
+    if (~(bokm & (farm | ballot(lt)))) {  // some lane undecided (rare): its root
       const bool sure = (bb >= 1.0e-10f && bb < 0x1p60f) && (gt || lt);
       far = sure ? gt : __builtin_sqrtf(q2) > bb;
+      farm = ballot(far);
     }
     bool pass = has && !far;
-    uint64_t passm = ballot(lane < total - base) & ~ballot(far);  // ballot(pass), compares' masks
+    uint64_t passm = ballot(lane < total - base) & ~farm;  // ballot(pass)
     if (!passm) continue;
     const float dax = (va * ca) * dt, day = (va * sa) * dt, dbx = (vb * cb) * dt, dby = (vb * sb) * dt;
     // a's v axis (the SAT's second edge normal) first: a pair separated on it both as it stands
