@@ -873,6 +873,9 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   const int tl_old = v.tl;
   const bool mid = v.ln != v.tl;
   const bool fire = actor && !mid && (LANE_CHANGE_DELAY < v.tmr);  // utils.do_every
+  // (wave masks from the compares' own masks: a ballot of a compound bool costs two VALU)
+  const uint64_t actm = pres & ~1ull & ~ballot(v.crashed);  // ballot(actor)
+  const uint64_t firem = actm & ~ballot(v.ln != v.tl) & ballot(LANE_CHANGE_DELAY < v.tmr);
   if (fire) v.tmr = 0.0f;
 
   // Road.neighbour_vehicles on lanes ln-1, ln, ln+1 (slot s <-> lane ln-1+s)
@@ -921,23 +924,32 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   // gain -- rarely any in a frame; the decision is upstream's.
   SEC(sp, 2);
   int ntl = v.tl;
+  // (every lane evaluates both sides when any lane fires -- a lane without a front on a side,
+  // or outside the lanes, reads a_free -- and the lane's own tests mask the result)
   bool gain[2] = {false, false};
-  if (fire && !(kSkip & 1)) {
+  uint64_t gainm = 0ull;
+  // the side-independent tests, once (a ballot of a compare used again under another branch
+  // re-materialises too)
+  const uint64_t basem = firem & ballot(0.0f <= v.x) & ballot(v.x < ROAD_LENGTH + LANE_VEH_LEN) &
+                         ~ballot(hm_absf(v.spd) < 1.0f);
+  if (basem && !(kSkip & 1)) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int c = v.ln - 1 + 2 * q;
       const int s = 2 * q;
-      if (c < 0 || c >= lanes) continue;
-      if (!(hm_absf(lane_lat(v.y, c)) <= 2.0f * LANE_WIDTH && 0.0f <= v.x &&
-            v.x < ROAD_LENGTH + LANE_VEH_LEN))
-        continue;  // is_reachable_from
-      if (hm_absf(v.spd) < 1.0f) continue;
       const float spa = idm_with_front(a_free, v.spd, v.x, ch, sh, vvx, vvy, fi[s] >= 0, np_x[q],
                                        np_vx[q], np_vy[q]);
-      gain[q] = !((spa - self_a) < LANE_CHANGE_MIN_ACC_GAIN);
+      const bool in_lanes = c >= 0 && c < lanes;
+      const bool reach = hm_absf(lane_lat(v.y, c)) <= 2.0f * LANE_WIDTH && 0.0f <= v.x &&
+                         v.x < ROAD_LENGTH + LANE_VEH_LEN;  // is_reachable_from
+      const bool slow = hm_absf(v.spd) < 1.0f;
+      const bool loss = (spa - self_a) < LANE_CHANGE_MIN_ACC_GAIN;
+      gain[q] = fire && in_lanes && reach && !slow && !loss;
+      gainm |= basem & ballot(c >= 0) & ballot(c < lanes) &
+               ballot(hm_absf(lane_lat(v.y, c)) <= 2.0f * LANE_WIDTH) & ~ballot(loss);
     }
   }
-  if (wave_any(gain[0] || gain[1])) {
+  if (gainm) {
     // upstream tries left, then right, and a passing right side overrides the left: so each
     // lane first evaluates the side that decides if it passes -- the right where it gains, else
     // the left -- in one pass over the lanes (one new-follower IDM, a pow, instead of two), and
@@ -969,8 +981,6 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
   // abort an ongoing lane change if another car targets the same lane within its desired gap,
   // in road order (lower indices already final, higher ones at their frame-start target)
   int tl_cur = ntl;
-  // (wave masks from the compares' own masks: a ballot of a compound bool costs two VALU)
-  const uint64_t actm = pres & ~1ull & ~ballot(v.crashed);  // ballot(actor)
   uint64_t cm = (kSkip & 8) ? 0ull : actm & ballot(v.ln != v.tl);  // actor && mid
   // a lane can trigger an abort only while its visible target is not its own lane (vis == tj
   // and ln != tj), under either visibility; aborts only ever clear that, so this superset holds
