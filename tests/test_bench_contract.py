@@ -82,10 +82,11 @@ def test_per_kernel_roofline_reproduces_from_the_cited_rocprof_file():
                       .read().strip().splitlines()[-1])
     roof = line["roofline"]
     kf = bench.ppo_kernel_flops_per_sample(60, 256)
-    got = bench.rocprof_per_kernel((1, 4096, 32, 256), kf, roof["rows_per_launch"],
-                                   roof["avg_launch_us"])
+    got = bench.rocprof_per_kernel((1, 4096, 32, 256, "none", "sorted"), kf,
+                                   roof["rows_per_launch"], roof["avg_launch_us"])
     assert got is not None and got["source"].endswith("kernel_stats_c1.txt")
     assert all(got[k]["us"] > 0 for k in ("ppo_rows", "ppo_wgrad", "ppo_wsum", "ppo_adam"))
     assert abs(got["sum_us"] / roof["avg_launch_us"] - 1.0) < 0.02
     # no summary of an unmeasured workload
-    assert bench.rocprof_per_kernel((3, 8192, 128, 256), kf, 1, 1.0) is None
+    assert bench.rocprof_per_kernel((3, 8192, 128, 256, "none", "sorted"), kf, 1, 1.0) is None
+    assert bench.rocprof_per_kernel((1, 4096, 32, 256, "rope", "shuffled"), kf, 1, 1.0) is None
