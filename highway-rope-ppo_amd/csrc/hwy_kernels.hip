@@ -494,9 +494,10 @@ __device__ __forceinline__ void write_pe_row(const float* vals, int F, int kind,
 
 // KinematicObservation.observe + fused wrapper for the env of this wave.
 // ch / sh: hm_cosf / hm_sinf of v.h (the step carries them from the last frame)
+// lds_key: WAVE 64-bit words of per-wave LDS scratch (the distance ranking)
 __device__ void observe_wave(const hwy_config& C, int lane, const Veh& v, float ch, float sh,
                              int step, uint64_t seed, const float* pe_table, float* obs_env,
-                             int fout, int* lds_vor, int* lds_inv) {
+                             int fout, int* lds_vor, int* lds_inv, unsigned long long* lds_key) {
   const int V = C.vehicles_count + 1;
   const int N = C.obs_vehicles, F = C.n_features;
   const float ex = rdlf(v.x, 0), ey = rdlf(v.y, 0), eh = rdlf(v.h, 0), espd = rdlf(v.spd, 0);
@@ -511,20 +512,22 @@ __device__ void observe_wave(const hwy_config& C, int lane, const Veh& v, float 
   if (C.order == HWY_ORDER_SORTED && (kSkip & 64)) {
     rank = __popcll(em & ((1ull << lane) - 1ull));
   } else if (C.order == HWY_ORDER_SORTED) {
-    float key = hm_absf(v.x - ex);
+    // rank = #{eligible k : |dx_k| < |dx| or (|dx_k| == |dx| and k < lane)}: the bits of |dx|
+    // (non-negative: their order is the value order) above the vehicle index make one 64-bit
+    // key per vehicle, so a single compare orders by distance and breaks ties by index; an
+    // ineligible vehicle holds ~0 and is never below an eligible one.  The keys go through LDS
+    // and every lane reads them at the same address (broadcast): two VALU per vehicle
+    const unsigned long long ck =
+        elig ? ((unsigned long long)hm_f2bits(hm_absf(v.x - ex)) << 32) | (uint32_t)lane : ~0ull;
+    lds_key[lane] = ck;
+    wave_lds_sync();
     rank = 0;
-    // four vehicles per round: their keys are read first, then compared (no branch per vehicle)
-    for (int k0 = 1; k0 < V; k0 += 4) {
-      float kk[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) kk[u] = rdlf(key, min(k0 + u, WAVE - 1));
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = k0 + u;
-        const bool ek = k < V && ((em >> k) & 1ull);
-        rank += (ek && (kk[u] < key || (kk[u] == key && k < lane))) ? 1 : 0;
-      }
+    for (int k0 = 0; k0 < V; k0 += 2) {
+      const unsigned long long k_a = lds_key[k0], k_b = lds_key[k0 + 1];
+      rank += k_a < ck ? 1 : 0;
+      rank += k_b < ck ? 1 : 0;  // lane k0 + 1 >= V is not present: ~0
     }
+    wave_lds_sync();
   } else {
     rank = __popcll(em & ((1ull << lane) - 1ull));
   }
@@ -1319,7 +1322,8 @@ hwy_step_kernel(StepParams P) {
   }
   SEC(sp, 12);
   observe_wave(C, lane, v, cos_h, sin_h, step, seed, P.pe_table,
-               P.obs + (size_t)e * C.obs_vehicles * P.fout, P.fout, lds_vor[w], lds_inv[w]);
+               P.obs + (size_t)e * C.obs_vehicles * P.fout, P.fout, lds_vor[w], lds_inv[w],
+               lds_coll[w].imx);  // the collision pass's scratch is free after the frames
   SEC(sp, 13);
   store_veh(st, fstride, idx, lane, V, v, ro.rk);
   store_env_words(st, fstride, idx, lane, step, episode, seed, rdlf(v.aacc, 0), rdlf(v.asteer, 0),
@@ -1334,6 +1338,7 @@ hwy_step_kernel(StepParams P) {
 __global__ void __launch_bounds__(256) hwy_reset_kernel(StepParams P) {
   __shared__ int lds_vor[ENVS_PER_BLOCK][WAVE];
   __shared__ int lds_inv[ENVS_PER_BLOCK][WAVE];
+  __shared__ unsigned long long lds_key[ENVS_PER_BLOCK][WAVE];
   const hwy_config& C = P.cfg;
   const int lane = threadIdx.x & (WAVE - 1);
   const int w = threadIdx.x / WAVE;
@@ -1348,7 +1353,8 @@ __global__ void __launch_bounds__(256) hwy_reset_kernel(StepParams P) {
   reset_wave(C, lane, seed, v);
   if (P.obs)
     observe_wave(C, lane, v, 1.0f, 0.0f, 0, seed, P.pe_table,
-                 P.obs + (size_t)e * C.obs_vehicles * P.fout, P.fout, lds_vor[w], lds_inv[w]);
+                 P.obs + (size_t)e * C.obs_vehicles * P.fout, P.fout, lds_vor[w], lds_inv[w],
+                 lds_key[w]);
   store_veh(P.state, fstride, idx, lane, V, v, reset_order_pos(lane, V));
   store_env_words(P.state, fstride, idx, lane, 0, 0, seed, 0.0f, 0.0f, 0.0f);
 }
