@@ -4,8 +4,8 @@
 # gpurun_out/measure); copy what is judged into profiles/<round>/measure/.
 #   PART=tests  GPU test suite (TESTS="tests/x.py ..." limits it) + smoke + the default bench line
 #   PART=lines  bench lines: configs[1] at T = 128, configs[2]-[4], configs[4]'s PE / hidden points
-#   PART=prof   rocprofv3 --kernel-trace --stats of the configs[1] / configs[2] benches
-#               -> kernel_stats_c<C>.txt (tools/summarize_stats.py)
+#   PART=prof   rocprofv3 --kernel-trace --stats of the configs[1] (T = 32 and 128) / configs[2]
+#               benches -> kernel_stats_c<C>.txt (tools/summarize_stats.py)
 #   PART=all    (default) the three in order
 set -o pipefail
 OUT=${OUT:-gpurun_out/measure}
@@ -49,10 +49,12 @@ lines() {
 prof() {
   local c S
   cd /tmp && export TMPDIR=/tmp && cd "$R"
-  for c in 1 2; do
+  local spec
+  for spec in "1" "2" "1 --rollout 128"; do
+    c=$(echo "$spec" | tr -d ' -')
     step rocprof c$c
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c$c" -o run -- python3 bench.py \
-      --config $c --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/bench_prof_c$c.log" 2>&1 || { tail -20 "$OUT/bench_prof_c$c.log"; return 1; }
+      --config $spec --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/bench_prof_c$c.log" 2>&1 || { tail -20 "$OUT/bench_prof_c$c.log"; return 1; }
     S=$(ls "$OUT"/prof_c$c/run_kernel_stats.csv "$OUT"/prof_c$c/*/run_kernel_stats.csv \
           "$OUT"/prof_c$c/run_results.db "$OUT"/prof_c$c/*/run_results.db 2>/dev/null | head -1)
     python3 tools/summarize_stats.py "$S" 16 > "$OUT/kernel_stats_c$c.txt" && head -8 "$OUT/kernel_stats_c$c.txt"
