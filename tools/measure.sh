@@ -59,6 +59,7 @@ prof() {
           "$OUT"/prof_c$c/run_results.db "$OUT"/prof_c$c/*/run_results.db 2>/dev/null | head -1)
     python3 tools/summarize_stats.py "$S" 16 > "$OUT/kernel_stats_c$c.txt" && head -8 "$OUT/kernel_stats_c$c.txt"
     grep '^{' "$OUT/bench_prof_c$c.log" | tail -1 > "$OUT/bench_prof_c$c.json"
+    rm -rf "$OUT/prof_c$c"  # the trace database (tens of MB); its summary is kept
   done
 }
 
