@@ -121,10 +121,13 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // ------------------------------------------------------------------------- section clocks
 // Development build only (make prof -> libhwy_prof.so): per-section shader-clock totals of the
-// step kernel, summed over waves, read back with hwy_debug_sections().
-#define HWY_NSEC 16
+// step kernel, accumulated per env (plain loads and stores by the env's own wave: one device
+// atomic per section and wave on shared counters serialised the launch's tail and inflated the
+// last sections several-fold) and summed over envs by hwy_debug_sections().
+#define HWY_NSEC 18
+#define HWY_NSEC_ENVS 16384
 #ifdef HWY_SECTION_PROFILE
-__device__ unsigned long long g_hwy_sections[HWY_NSEC];
+__device__ unsigned long long g_hwy_sections[HWY_NSEC_ENVS][HWY_NSEC];
 struct SecProf {
   uint64_t t;
   uint64_t acc[HWY_NSEC];
@@ -140,10 +143,10 @@ struct SecProf {
     (sp).acc[id] += _n - (sp).t;                         \
     (sp).t = _n;                                         \
   } while (0)
-#define SEC_FLUSH(sp, lane)                                                        \
-  do {                                                                             \
-    if ((lane) == 0)                                                               \
-      for (int _i = 0; _i < HWY_NSEC; ++_i) atomicAdd(&g_hwy_sections[_i], (sp).acc[_i]); \
+#define SEC_FLUSH(sp, lane, e)                                                \
+  do {                                                                        \
+    if ((lane) == 0 && (e) < HWY_NSEC_ENVS)                                   \
+      for (int _i = 0; _i < HWY_NSEC; ++_i) g_hwy_sections[e][_i] += (sp).acc[_i]; \
   } while (0)
 #else
 struct SecProf {};
@@ -153,8 +156,8 @@ struct SecProf {};
 #define SEC(sp, id) \
   do {              \
   } while (0)
-#define SEC_FLUSH(sp, lane) \
-  do {                      \
+#define SEC_FLUSH(sp, lane, e) \
+  do {                         \
   } while (0)
 #endif
 // Development builds (make prof / make waves -> libhwy_waves.so, tools/probe_waves.py):
@@ -1269,10 +1272,22 @@ hwy_step_kernel(StepParams P) {
   }
   // the ego's steering changes only here and to 0 on a crash (handled in frame_wave)
   const float tan_ego = rdlf(lane == 0 ? hm_tanf_sc(v.asteer) : 0.0f, 0);
-  for (int frame = 0; frame < frames; ++frame)
+  // Issue priority falls with progress through the frames (s_setprio 3, 2, 1, 0 from 6/15, 10/15
+  // and 13/15 of them): the SIMD's arbiter otherwise prefers its oldest wave, so a SIMD's four
+  // waves finished one after another and the last ran its final frames alone, with no other
+  // wave to hide its latency.  Lagging waves now catch up and the four finish together (the
+  // launch ends with the slowest SIMD).  Scheduling only: the same instructions and results.
+  for (int frame = 0; frame < frames; ++frame) {
+    const int f15 = 15 * frame;
+    if (f15 < 6 * frames) __builtin_amdgcn_s_setprio(3);
+    else if (f15 < 10 * frames) __builtin_amdgcn_s_setprio(2);
+    else if (f15 < 13 * frames) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
     frame_wave(C, lane, v, dt, tan_ego, ro, cos_h, sin_h, lds_coll[w], sp, pres);
+  }
+  __builtin_amdgcn_s_setprio(0);  // the reward, observation and stores at the lowest priority
   step += 1;
-  SEC(sp, 11);
+  SEC(sp, 16);
 
   // HighwayEnv._reward / _is_terminated / _is_truncated on the ego (lane 0)
   float rew = 0.0f;
@@ -1326,13 +1341,14 @@ hwy_step_kernel(StepParams P) {
                lds_coll[w].imx);  // the collision pass's scratch is free after the frames
   SEC(sp, 13);
   store_veh(st, fstride, idx, lane, V, v, ro.rk);
+  SEC(sp, 17);
   store_env_words(st, fstride, idx, lane, step, episode, seed, rdlf(v.aacc, 0), rdlf(v.asteer, 0),
                   ep_return);
   SEC(sp, 14);
   WAVE_T(e, lane, 1, __builtin_amdgcn_s_memtime());
   WAVE_T(e, lane, 4, __builtin_amdgcn_s_memrealtime());
   WAVE_T(e, lane, 2, (unsigned long long)done | WAVE_HWID());
-  SEC_FLUSH(sp, lane);
+  SEC_FLUSH(sp, lane, e);
 }
 
 __global__ void __launch_bounds__(256) hwy_reset_kernel(StepParams P) {
@@ -1520,12 +1536,22 @@ extern "C" int hwy_debug_wave_times(unsigned long long* out, int n) {
 #endif
 #ifdef HWY_SECTION_PROFILE
 // development build only: copy out (and optionally clear) the section clock totals
+// development build only: the per-env totals themselves ([n][HWY_NSEC], n <= HWY_NSEC_ENVS)
+extern "C" int hwy_debug_sections_env(unsigned long long* out, int n) {
+  if (n > HWY_NSEC_ENVS) n = HWY_NSEC_ENVS;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hwy_sections),
+                             sizeof(unsigned long long) * HWY_NSEC * n) == hipSuccess ? 0 : -2;
+}
 extern "C" int hwy_debug_sections(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hwy_sections), sizeof(g_hwy_sections)) != hipSuccess)
-    return -2;
+  static unsigned long long h[HWY_NSEC_ENVS][HWY_NSEC];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_hwy_sections), sizeof(h)) != hipSuccess) return -2;
+  for (int i = 0; i < HWY_NSEC; ++i) out[i] = 0;
+  for (int e = 0; e < HWY_NSEC_ENVS; ++e)
+    for (int i = 0; i < HWY_NSEC; ++i) out[i] += h[e][i];
   if (reset) {
-    unsigned long long z[HWY_NSEC] = {0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_hwy_sections), z, sizeof(z)) != hipSuccess) return -2;
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_hwy_sections)) != hipSuccess) return -2;
+    if (hipMemset(p, 0, sizeof(h)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return -2;
   }
   return 0;
 }

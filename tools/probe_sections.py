@@ -16,14 +16,14 @@ NAMES = {15: "load", 0: "frame head", 9: "road order (frame 0)", 1: "neighbours"
          3: "MOBIL", 4: "abort check", 5: "target IDM+steering", 6: "kinematics",
          7: "post-move order", 10: "collision candidates", 8: "pre-check+SAT", 11: "reward",
          12: "reset", 13: "observe",
-         14: "store"}
+         14: "store (env words)", 16: "frames exit", 17: "store (vehicles)"}
 E = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 env = HighwayVecEnv(HIGHWAY_CONFIG, num_envs=E, device="cuda:0", autoreset=True, seed_base=42)
 env.reset()
 a = torch.zeros(E, 2, device="cuda:0")
 L = native.lib()
 L.hwy_debug_sections.argtypes = [ctypes.c_void_p, ctypes.c_int]
-buf = (ctypes.c_ulonglong * 16)()
+buf = (ctypes.c_ulonglong * 18)()
 for _ in range(5):
     env.step(a)
 torch.cuda.synchronize()
