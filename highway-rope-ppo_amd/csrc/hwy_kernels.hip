@@ -1279,12 +1279,10 @@ hwy_step_kernel(StepParams P) {
   // launch ends with the slowest SIMD).  Scheduling only: the same instructions and results.
   for (int frame = 0; frame < frames; ++frame) {
     const int f15 = 15 * frame;
-#ifndef HWY_NO_FRAME_PRIO  // (development A/B builds only: without)
     if (f15 < 6 * frames) __builtin_amdgcn_s_setprio(3);
     else if (f15 < 10 * frames) __builtin_amdgcn_s_setprio(2);
     else if (f15 < 13 * frames) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
-#endif
     frame_wave(C, lane, v, dt, tan_ego, ro, cos_h, sin_h, lds_coll[w], sp, pres);
   }
   __builtin_amdgcn_s_setprio(0);  // the reward, observation and stores at the lowest priority
