@@ -125,7 +125,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // atomic per section and wave on shared counters serialised the launch's tail and inflated the
 // last sections several-fold) and summed over envs by hwy_debug_sections().
 #define HWY_NSEC 18
-#define HWY_NSEC_ENVS 16384
+#define HWY_NSEC_ENVS 32768  // the largest profiled workload (configs[4]: 32,768 envs per GPU)
 #ifdef HWY_SECTION_PROFILE
 __device__ unsigned long long g_hwy_sections[HWY_NSEC_ENVS][HWY_NSEC];
 struct SecProf {
@@ -145,8 +145,9 @@ struct SecProf {
   } while (0)
 #define SEC_FLUSH(sp, lane, e)                                                \
   do {                                                                        \
-    if ((lane) == 0 && (e) < HWY_NSEC_ENVS)                                   \
-      for (int _i = 0; _i < HWY_NSEC; ++_i) g_hwy_sections[e][_i] += (sp).acc[_i]; \
+    if ((lane) == 0) /* envs past the cap fold onto env mod cap: none is dropped */ \
+      for (int _i = 0; _i < HWY_NSEC; ++_i)                                   \
+        g_hwy_sections[(e) % HWY_NSEC_ENVS][_i] += (sp).acc[_i];             \
   } while (0)
 #else
 struct SecProf {};
@@ -1538,6 +1539,7 @@ extern "C" int hwy_debug_wave_times(unsigned long long* out, int n) {
 // development build only: copy out (and optionally clear) the section clock totals
 // development build only: the per-env totals themselves ([n][HWY_NSEC], n <= HWY_NSEC_ENVS)
 extern "C" int hwy_debug_sections_env(unsigned long long* out, int n) {
+  if (!out || n < 0) return -1;
   if (n > HWY_NSEC_ENVS) n = HWY_NSEC_ENVS;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hwy_sections),
                              sizeof(unsigned long long) * HWY_NSEC * n) == hipSuccess ? 0 : -2;

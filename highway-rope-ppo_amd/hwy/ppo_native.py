@@ -404,17 +404,22 @@ class FusedPPO:
         args = [self._args(states, pre_tanh, old_lp, adv, ret, perm.data_ptr() + i * mb * 8)
                 for i in range(nmb)]
         self._last_args = args
+        # the tensors behind args' raw addresses stay referenced while the args are kept
+        # (time_kernels replays them later)
+        self._last_inputs = (states, pre_tanh, old_lp, adv, ret, perm)
         self.counters[1].zero_()
         # the weight tile image the row kernel streams: params may have been written since the
         # last update (checkpoint load, torch optimizer); hwy_ppo_optimizer keeps it in step
         self.sync_params(args[0])
         if not self.use_graphs:
             for _ in range(epochs):
+                ev = self._epoch_event()
                 for a in args:
                     self._fwd_bwd(a)
                     if self.group is not None:
                         self._allreduce()
                     self._opt(a)
+                self._epoch_event(ev)
             self._tiles_version = self._param_versions()
             return self.metrics
         if self._graphs is None or self._bound_key != key:
@@ -439,19 +444,28 @@ class FusedPPO:
         """Average microseconds per launch of each kernel of the minibatch step (ppo_rows,
         ppo_wgrad, ppo_wsum, ppo_adam) on the last update's first minibatch, each as a HIP graph
         of `reps` back-to-back launches (hwy_ppo_time_kernels), and of an empty kernel
-        (`launch_floor`: the per-launch cost a kernel-trace duration leaves out).  A measurement aid for bench.py,
-        run after its timed region: the Adam launches update the weights and moments as training
-        steps do, and metrics row 0 is overwritten.  None before the first run()."""
+        (`launch_floor`: the per-launch cost a kernel-trace duration leaves out).  A measurement
+        aid for bench.py, run after its timed region.  The training state is left as it was
+        (ADVICE r5): the repeated Adam launches step the weights, moments and tile image with one
+        gradient, so params, Adam moments, counters and metrics are snapshotted before and put
+        back after, and the tile image is rebuilt from the restored params.  None before the
+        first run()."""
         args = getattr(self, "_last_args", None)
         if not args:
             return None
+        # the last run's inputs are held with its args, so the addresses are still live
         a = PpoArgs.from_buffer_copy(args[0])
         a.grads_modified = 0  # this rank's own kernels only (no all-reduce between them)
+        saved = [t.clone() for t in (self.flat, self.m, self.v, self.counters, self.metrics)]
         self.counters[1].zero_()
         us = (ctypes.c_float * 5)()
         check(self.L.hwy_ppo_time_kernels(ctypes.byref(a), stream_ptr(), max(1, int(reps)), us),
               "hwy_ppo_time_kernels")
-        self.counters[1].zero_()
+        with torch.no_grad():
+            for dst, src in zip((self.flat, self.m, self.v, self.counters, self.metrics), saved):
+                dst.copy_(src)
+        self.grads.zero_()
+        self.sync_params(a)
         self._tiles_version = self._param_versions()
         return dict(zip(self.KERNELS + ("launch_floor",), (float(u) for u in us)))
 

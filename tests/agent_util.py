@@ -9,26 +9,34 @@ import torch
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def load():
+def load(bench: bool = False):
+    """(arrays, meta) of the reference's golden updates: ppo_agent.npz (upd_a / upd_b, small) or,
+    bench=True, ppo_agent_bench.npz (upd_c1 / upd_c2 / upd_c4: the benched learners at the
+    reference's 2,048-sample, 8-epoch, batch-64 update; make_golden.py bench)."""
+    if bench:
+        return (np.load(os.path.join(GOLD, "ppo_agent_bench.npz")),
+                json.load(open(os.path.join(GOLD, "golden_bench_meta.json"))))
     return np.load(os.path.join(GOLD, "ppo_agent.npz")), json.load(open(os.path.join(GOLD, "golden_meta.json")))
 
 
-def replay_update(name, device, gae_fn=None, use_graphs=False):
+def replay_update(name, device, gae_fn=None, use_graphs=False, bench=False):
     """Build PPOAgent with the golden initial weights and memory, run update() with the same
     minibatch permutation (global numpy RNG seeded as the generator did), return (agent, metrics)."""
     from ppo.agent import PPOAgent
 
-    g, meta = load()
+    g, meta = load(bench)
     m = meta["agent"][name]
     agent = PPOAgent(m["state_dim"], 2, lr=m["lr"], epochs=m["epochs"], batch_size=m["batch_size"],
                      hidden_dim=m["hidden_dim"], device=torch.device(device), use_graphs=use_graphs)
     sd = {k[len(name) + 6:]: torch.as_tensor(g[k]) for k in g.files if k.startswith(f"{name}_init_")}
     agent.actor_critic.load_state_dict(sd)
     n = m["n"]
+    a = {k: g[f"{name}_{k}"] for k in ("states", "actions", "pre_tanh", "rewards", "log_probs",
+                                        "dones", "values")}  # each npz member decompressed once
     for t in range(n):
-        agent.memory.store(g[f"{name}_states"][t], g[f"{name}_actions"][t], g[f"{name}_pre_tanh"][t],
-                           float(g[f"{name}_rewards"][t]), None, float(g[f"{name}_log_probs"][t]),
-                           bool(g[f"{name}_dones"][t]), g[f"{name}_values"][t])
+        agent.memory.store(a["states"][t], a["actions"][t], a["pre_tanh"][t],
+                           float(a["rewards"][t]), None, float(a["log_probs"][t]),
+                           bool(a["dones"][t]), a["values"][t])
     if gae_fn is not None:
         agent.memory.compute_advantages = gae_fn(agent.memory)
     np.random.seed(m["np_seed"])

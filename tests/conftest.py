@@ -13,6 +13,27 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running")
 
 
+# Hot-path parity first: under `pytest -x` a harness or format check must
+# never gate the env / kernel / PE-wrapper / fused-PPO parity tests, so those modules run ahead
+# of the agent, rollout, bench, dist and runner modules.  Within a module the file order holds.
+_FIRST = ("test_env_parity_gpu", "test_kernels_gpu", "test_wrappers_gpu", "test_ppo_fused_gpu",
+          "test_agent_gpu", "test_rollout_graph_gpu", "test_dist_fused_gpu")
+_LAST = ("test_bench_gpu", "test_bench_dist_gpu", "test_runner_dist_gpu")
+
+
+def _rank(item) -> int:
+    mod = os.path.splitext(os.path.basename(str(item.fspath)))[0]
+    if mod in _FIRST:
+        return _FIRST.index(mod)
+    if mod in _LAST:
+        return len(_FIRST) + 1 + _LAST.index(mod)
+    return len(_FIRST)
+
+
+def pytest_collection_modifyitems(session, config, items):
+    items.sort(key=_rank)  # stable: file and definition order kept inside each rank
+
+
 # development A/B only (tools/ab.sh TESTS=1): run the suite against a variant library build
 if os.environ.get("HWY_LIB"):
     import hwy.native as _native

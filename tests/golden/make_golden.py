@@ -224,12 +224,96 @@ def gen_agent(rng):
     return out, meta
 
 
-def main():
+BENCH_UPDATES = {
+    # name: (state_dim, hidden_dim, epochs, batch_size, n) -- the reference's update at the
+    # benched learners: configs[1]'s cell (sd 60 / h256), configs[2]'s
+    # (sd 120 / h256) and configs[4]'s widest (sd 120 / h512), each at the reference's own
+    # update statistics: 2,048 samples, 8 epochs of 32 minibatches of 64 (256 Adam steps)
+    "upd_c1": (60, 256, 8, 64, 2048),
+    "upd_c2": (120, 256, 8, 64, 2048),
+    "upd_c4": (120, 512, 8, 64, 2048),
+}
+
+
+def gen_bench_updates():
+    """One full reference PPOAgent.update (ppo/agent.py:196-308) per BENCH_UPDATES entry, with
+    its own generator (seed 20261018) so the older fixtures' draws are untouched.  Stored: the
+    initial weights, the memory (states, pre-tanh, actions, log-probs, rewards, dones, values),
+    the minibatch permutation, the final weights and the metrics dict."""
+    import torch
+
+    from ppo.agent import PPOAgent
+
+    rng = np.random.default_rng(20261018)
+    out, meta = {}, {}
+    for name, (sd, h, epochs, bs, n) in BENCH_UPDATES.items():
+        torch.manual_seed(29)
+        agent = PPOAgent(sd, 2, lr=3e-4, epochs=epochs, batch_size=bs, hidden_dim=h)
+        init = {k: v.detach().clone().numpy() for k, v in agent.actor_critic.state_dict().items()}
+        # Kinematics-like inputs: normalised features in [-1, 1], a share of zero-padded rows
+        S = np.clip(rng.normal(scale=0.4, size=(n, sd)), -1, 1).astype(np.float32)
+        S[rng.random((n, sd)) < 0.15] = 0.0
+        Zs = rng.normal(size=(n, 2)).astype(np.float32) * 0.7
+        with torch.no_grad():
+            m_, s_, v_ = agent.actor_critic.forward(torch.from_numpy(S))
+            dist = torch.distributions.Normal(m_, s_)
+            zt = torch.from_numpy(Zs)
+            at = torch.tanh(zt)
+            lp_ = (dist.log_prob(zt) - torch.log1p(-at.pow(2) + 1e-6)).sum(-1)
+        R = rng.uniform(0, 1, size=n).astype(np.float32)
+        D = rng.random(n) < 0.01
+        for t in range(n):
+            agent.memory.store(S[t], at[t].numpy(), Zs[t], float(R[t]), None,
+                               float(lp_[t].item()), bool(D[t]), v_[t].numpy()[0])
+        np.random.seed(321)
+        perm_rng = np.random.get_state()
+        metrics = agent.update(last_value=0.5)
+        np.random.set_state(perm_rng)
+        idx = np.arange(n, dtype=np.int64)
+        np.random.shuffle(idx)
+        out[f"{name}_perm"] = idx
+        for k, v in init.items():
+            out[f"{name}_init_{k}"] = v
+        for k, v in agent.actor_critic.state_dict().items():
+            out[f"{name}_final_{k}"] = v.detach().numpy()
+        out[f"{name}_states"] = S
+        out[f"{name}_pre_tanh"] = Zs
+        out[f"{name}_actions"] = at.numpy()
+        out[f"{name}_log_probs"] = lp_.numpy().astype(np.float32)
+        out[f"{name}_rewards"] = R
+        out[f"{name}_dones"] = D.astype(np.uint8)
+        out[f"{name}_values"] = v_[:, 0].numpy()
+        meta[name] = dict(state_dim=sd, hidden_dim=h, epochs=epochs, batch_size=bs, n=n, lr=3e-4,
+                          last_value=0.5, np_seed=321, metrics=metrics)
+        print(name, metrics, flush=True)
+    return out, meta
+
+
+def _shim_path():
     tmp = tempfile.mkdtemp(prefix="gym_shim_")
     os.makedirs(os.path.join(tmp, "gymnasium"))
     with open(os.path.join(tmp, "gymnasium", "__init__.py"), "w") as f:
         f.write(_SHIM)
     sys.path[:0] = [REF, tmp]
+
+
+def main_bench():
+    """python tests/golden/make_golden.py bench -> ppo_agent_bench.npz + golden_bench_meta.json"""
+    _shim_path()
+    import torch
+
+    torch.set_num_threads(1)
+    out, meta = gen_bench_updates()
+    np.savez_compressed(os.path.join(OUT, "ppo_agent_bench.npz"), **out)
+    with open(os.path.join(OUT, "golden_bench_meta.json"), "w") as f:
+        json.dump({"agent": meta, "generator": "tests/golden/make_golden.py bench",
+                   "reference": "DhruvDh/highway-rope-ppo @ 2025-05-23",
+                   "torch": torch.__version__, "numpy": np.__version__,
+                   "torch_threads": 1}, f, indent=2)
+
+
+def main():
+    _shim_path()
     import torch
 
     torch.set_num_threads(1)
@@ -249,4 +333,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["bench"]:
+        main_bench()
+    else:
+        main()

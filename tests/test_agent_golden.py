@@ -45,6 +45,20 @@ def test_ppo_update_matches_reference(name):
     compare(agent, metrics, g, m, name, wtol=2e-5)
 
 
+@pytest.mark.parametrize("name", ["upd_c1", "upd_c2", "upd_c4"])
+def test_ppo_update_matches_reference_at_bench_learners(name):
+    """The reference's update at the benched learners (ppo_agent_bench.npz: sd 60 / h256,
+    sd 120 / h256, sd 120 / h512; 2,048 samples, 8 epochs x 32 minibatches of 64) replayed by
+    this build's torch learner on the CPU: final weights and metrics bit for bit, so the golden
+    fixtures the GPU test replays (test_fused_update_replays_reference_golden_bench) pin this
+    build's own update semantics exactly."""
+    agent, metrics, g, m = replay_update(name, "cpu", gae_fn=oracle_gae, bench=True)
+    for k, v in agent.actor_critic.state_dict().items():
+        np.testing.assert_array_equal(v.detach().numpy(), g[f"{name}_final_{k}"], err_msg=k)
+    for k, want in m["metrics"].items():
+        assert metrics[k] == want, (k, metrics[k], want)
+
+
 def test_checkpoint_roundtrip(tmp_path):
     from ppo.agent import PPOAgent
 

@@ -329,6 +329,87 @@ def test_fused_update_replays_reference_golden(graphs):
         assert abs(metrics[k] - want) <= 1e-4 * max(1.0, abs(want)), (k, metrics[k], want)
 
 
+def _replay_bench_golden(name, backend, graphs):
+    """The reference's golden update `name` (tests/golden/ppo_agent_bench.npz) through
+    PPOAgent.update_rollout on the GPU: (agent, metrics, arrays, meta)."""
+    from agent_util import load
+    from ppo.agent import PPOAgent, RolloutBuffer
+
+    g, meta = load(bench=True)
+    m = meta["agent"][name]
+    n, S = m["n"], m["state_dim"]
+    agent = PPOAgent(S, 2, lr=m["lr"], epochs=m["epochs"], batch_size=m["batch_size"],
+                     hidden_dim=m["hidden_dim"], device=DEV, use_graphs=graphs, backend=backend)
+    sd = {k[len(name) + 6:]: torch.as_tensor(g[k]) for k in g.files if k.startswith(f"{name}_init_")}
+    agent.actor_critic.load_state_dict(sd)
+    buf = RolloutBuffer(n, 1, S, 2, DEV)
+    f = lambda k: torch.as_tensor(np.asarray(g[f"{name}_{k}"], np.float32), device=DEV)  # noqa: E731
+    buf.states[:n].copy_(f("states").view(n, 1, S))
+    buf.actions.copy_(f("actions").view(n, 1, 2))
+    buf.pre_tanh.copy_(f("pre_tanh").view(n, 1, 2))
+    buf.log_probs.copy_(f("log_probs").view(n, 1))
+    buf.values.copy_(f("values").view(n, 1))
+    buf.rewards.copy_(f("rewards").view(n, 1))
+    buf.dones.copy_(torch.as_tensor(np.asarray(g[f"{name}_dones"], np.uint8), device=DEV).view(n, 1))
+    perm = torch.as_tensor(np.asarray(g[f"{name}_perm"], np.int64), device=DEV)
+    last = torch.tensor([m["last_value"]], dtype=torch.float32, device=DEV)
+    metrics = agent.update_rollout(buf, last, perm=perm)
+    return agent, metrics, g, m
+
+
+def _rel_err(agent, g, name):
+    """Per parameter: ||W - W_ref|| / ||W_ref|| against the golden final weights."""
+    out = {}
+    for k, v in agent.actor_critic.state_dict().items():
+        want = np.asarray(g[f"{name}_final_{k}"], np.float64)
+        d = v.detach().cpu().numpy().astype(np.float64) - want
+        out[k] = float(np.linalg.norm(d) / max(np.linalg.norm(want), 1e-30))
+    return out
+
+
+_TORCH_GPU_DRIFT = {}
+
+
+@pytest.mark.parametrize("name,graphs", [("upd_c1", False), ("upd_c1", True), ("upd_c2", True),
+                                         ("upd_c4", True)])
+def test_fused_update_replays_reference_golden_bench(name, graphs):
+    """The reference's own update at the benched learners (generated by
+    tests/golden/make_golden.py bench from ppo/agent.py:196-308): 2,048 samples, 8 epochs x 32
+    minibatches of 64 = 256 Adam steps, at sd 60 / h256 (configs[1]'s cell), sd 120 / h256
+    (configs[2]) and sd 120 / h512 (configs[4]), replayed through the PRODUCT path
+    (update_rollout -> hwy_gae -> FusedPPO's HIP kernels, HIP graphs when graphs=True).
+
+    Over 256 Adam steps any fp32 implementation drifts from the reference's CPU run: Adam
+    normalises each element's step, so rounding-level gradient differences move near-zero
+    elements by up to lr per step, and a clip decision that flips on one sample changes that
+    sample's gradient outright.  On the CPU this build's torch learner replays the golden bit for
+    bit (test_agent_golden.py); PyTorch's own fp32 GPU learner (backend='torch': the reference's
+    algorithm on hipBLASLt GEMMs) drifts like the fused path (relative weight error up to 1e-2
+    at h512, tools/probe_golden_bench.py).  So the bound is relative to that drift, measured in
+    the same test: per parameter the fused path's relative error is at most 3x PyTorch-GPU's plus
+    2e-3, the whole model's at most 3x plus 1e-3 and below 5e-2, and every metric within 3x
+    PyTorch-GPU's deviation plus 1e-4 relative (clip fraction: 3x plus 2 / 2,048 samples)."""
+    if name not in _TORCH_GPU_DRIFT:
+        ta, tm, g, m = _replay_bench_golden(name, "torch", False)
+        assert getattr(ta, "_fused", None) is None
+        _TORCH_GPU_DRIFT[name] = (_rel_err(ta, g, name),
+                                  {k: abs(tm[k] - w) for k, w in m["metrics"].items()})
+    t_err, t_met = _TORCH_GPU_DRIFT[name]
+    agent, metrics, g, m = _replay_bench_golden(name, "hip", graphs)
+    F = agent._fused
+    assert F is not None and F.mb == 64 and F.nmb == m["n"] // 64
+    assert int(F.counters[0]) == m["epochs"] * (m["n"] // 64)
+    f_err = _rel_err(agent, g, name)
+    for k, e in f_err.items():
+        assert e <= 3 * t_err[k] + 2e-3, (k, e, t_err[k])
+    tot_f = float(np.sqrt(np.mean(np.square(list(f_err.values())))))
+    tot_t = float(np.sqrt(np.mean(np.square(list(t_err.values())))))
+    assert tot_f <= 3 * tot_t + 1e-3 and tot_f < 5e-2, (tot_f, tot_t)
+    for k, want in m["metrics"].items():
+        slack = 2.0 / m["n"] if k == "clip_fraction" else 1e-4 * max(1.0, abs(want))
+        assert abs(metrics[k] - want) <= 3 * t_met[k] + slack, (k, metrics[k], want, t_met[k])
+
+
 def test_ragged_update_rollout_replays_reference_golden():
     """'upd_b' (n 130, batch_size 50: minibatches 50 / 50 / 30) through update_rollout: the
     reference's get_batches partition with its short last minibatch is kept (no sample is
