@@ -16,6 +16,8 @@ struct hwy_handle {
   int fout;
   uint32_t* state;  // [HWY_NFIELDS][E][64]
   float* pe_table;  // [HWY_MAX_PE_TABLE]
+  int64_t* group_seed;  // [n_groups] (hwy_set_seed_groups), or null
+  int n_groups, group_envs, pe_group_stride;
 };
 
 static thread_local char g_err[512];
@@ -146,6 +148,7 @@ void hwy_destroy(hwy_handle* h) {
   (void)hipDeviceSynchronize();
   (void)hipFree(h->state);
   (void)hipFree(h->pe_table);
+  if (h->group_seed) (void)hipFree(h->group_seed);
   delete h;
 }
 
@@ -158,12 +161,47 @@ int hwy_set_pe_table(hwy_handle* h, const float* table_host, int n) {
   if (c.pe_kind == HWY_PE_RANK) need = c.obs_vehicles * c.d_embed;
   if (c.pe_kind == HWY_PE_DIST || c.pe_kind == HWY_PE_DIST1) need = c.d_embed / 2;
   if (c.pe_kind == HWY_PE_ROPE) need = c.d_embed / 2;
+  int stride = 0;
+  if (c.pe_kind == HWY_PE_RANK && h->n_groups > 0 && n == need * h->n_groups && n != need) {
+    stride = need;  // one RankPE table per experiment group
+    need = n;
+  }
   if (n != need) return fail(HWY_EINVAL, "pe table needs %d floats, got %d", need, n);
   if (n > HWY_MAX_PE_TABLE) return fail(HWY_EINVAL, "pe table too large (%d)", n);
   if (n == 0) return HWY_OK;
   (void)hipSetDevice(h->device);
   hipError_t e = hipMemcpy(h->pe_table, table_host, (size_t)n * sizeof(float), hipMemcpyHostToDevice);
   if (e != hipSuccess) return hip_fail(e, "hipMemcpy(pe_table)");
+  h->pe_group_stride = stride;
+  return HWY_OK;
+}
+
+int hwy_set_seed_groups(hwy_handle* h, const int64_t* seed_bases, int n_groups, int envs_per_group) {
+  if (!h) return fail(HWY_EINVAL, "handle is NULL");
+  (void)hipSetDevice(h->device);
+  if (n_groups == 0) {
+    if (h->group_seed) (void)hipFree(h->group_seed);
+    h->group_seed = nullptr;
+    h->n_groups = h->group_envs = h->pe_group_stride = 0;
+    return HWY_OK;
+  }
+  if (!seed_bases || n_groups < 0 || envs_per_group < 1 ||
+      (int64_t)n_groups * envs_per_group != h->cfg.num_envs)
+    return fail(HWY_EINVAL, "seed groups: %d groups x %d envs must cover num_envs %d", n_groups,
+                envs_per_group, h->cfg.num_envs);
+  int64_t* dev = nullptr;
+  hipError_t e = hipMalloc(&dev, (size_t)n_groups * sizeof(int64_t));
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc(group_seed)");
+  e = hipMemcpy(dev, seed_bases, (size_t)n_groups * sizeof(int64_t), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(dev);
+    return hip_fail(e, "hipMemcpy(group_seed)");
+  }
+  if (h->group_seed) (void)hipFree(h->group_seed);
+  h->group_seed = dev;
+  h->n_groups = n_groups;
+  h->group_envs = envs_per_group;
+  h->pe_group_stride = 0;  // a grouped RankPE table is set after the groups
   return HWY_OK;
 }
 
@@ -183,6 +221,9 @@ static StepParams params_of(hwy_handle* h) {
   p.state = h->state;
   p.pe_table = h->pe_table;
   p.fout = h->fout;
+  p.group_seed = h->group_seed;
+  p.group_envs = h->group_envs;
+  p.pe_group_stride = h->pe_group_stride;
   return p;
 }
 

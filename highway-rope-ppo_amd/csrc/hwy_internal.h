@@ -20,6 +20,11 @@ struct StepParams {
   const uint64_t* seeds;
   const uint8_t* mask;
   int fout;
+  // experiment groups (hwy_set_seed_groups): per-group seed bases, envs per group, and the
+  // floats between consecutive groups' PE tables (0: one table for all)
+  const int64_t* group_seed;
+  int group_envs;
+  int pe_group_stride;
 };
 
 extern "C" {

@@ -370,6 +370,21 @@ __device__ __forceinline__ uint64_t schedule_seed(const hwy_config& C, int e, in
                     C.seed_stride * (int64_t)episode);
 }
 
+// the seed of (env e, episode k): the handle's schedule, or its experiment group's
+// (hwy_set_seed_groups: group g = e / group_envs, l = e - g * group_envs)
+__device__ __forceinline__ uint64_t episode_seed(const StepParams& P, int e, int episode) {
+  const hwy_config& C = P.cfg;
+  if (!P.group_seed) return schedule_seed(C, e, episode);
+  const int g = e / P.group_envs, l = e - g * P.group_envs;
+  return (uint64_t)(P.group_seed[g] + (int64_t)C.env_offset + (int64_t)l + 1 +
+                    C.seed_stride * (int64_t)episode);
+}
+
+__device__ __forceinline__ const float* group_pe_table(const StepParams& P, int e) {
+  return P.pe_group_stride ? P.pe_table + (size_t)(e / P.group_envs) * P.pe_group_stride
+                           : P.pe_table;
+}
+
 // HighwayEnv._create_vehicles via Vehicle.create_random / IDMVehicle.randomize_behavior
 __device__ void reset_wave(const hwy_config& C, int lane, uint64_t seed, Veh& v) {
   const int V = C.vehicles_count + 1;
@@ -1328,7 +1343,7 @@ hwy_step_kernel(StepParams P) {
   SEC(sp, 11);
   if (done && C.autoreset) {
     episode += 1;
-    seed = schedule_seed(C, e, episode);
+    seed = episode_seed(P, e, episode);
     reset_wave(C, lane, seed, v);
     step = 0;
     ep_return = 0.0f;
@@ -1337,7 +1352,7 @@ hwy_step_kernel(StepParams P) {
     sin_h = 0.0f;
   }
   SEC(sp, 12);
-  observe_wave(C, lane, v, cos_h, sin_h, step, seed, P.pe_table,
+  observe_wave(C, lane, v, cos_h, sin_h, step, seed, group_pe_table(P, e),
                P.obs + (size_t)e * C.obs_vehicles * P.fout, P.fout, lds_vor[w], lds_inv[w],
                lds_coll[w].imx);  // the collision pass's scratch is free after the frames
   SEC(sp, 13);
@@ -1365,11 +1380,11 @@ __global__ void __launch_bounds__(256) hwy_reset_kernel(StepParams P) {
   const int V = C.vehicles_count + 1;
   const size_t fstride = (size_t)C.num_envs * WAVE;
   const uint32_t idx = (uint32_t)e * WAVE + lane;  // < 2^32: hwy_create bounds num_envs
-  const uint64_t seed = P.seeds ? P.seeds[e] : schedule_seed(C, e, 0);
+  const uint64_t seed = P.seeds ? P.seeds[e] : episode_seed(P, e, 0);
   Veh v;
   reset_wave(C, lane, seed, v);
   if (P.obs)
-    observe_wave(C, lane, v, 1.0f, 0.0f, 0, seed, P.pe_table,
+    observe_wave(C, lane, v, 1.0f, 0.0f, 0, seed, group_pe_table(P, e),
                  P.obs + (size_t)e * C.obs_vehicles * P.fout, P.fout, lds_vor[w], lds_inv[w],
                  lds_key[w]);
   store_veh(P.state, fstride, idx, lane, V, v, reset_order_pos(lane, V));

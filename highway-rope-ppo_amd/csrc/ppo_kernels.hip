@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 #include <cmath>
@@ -1535,7 +1536,7 @@ struct ActArgs {
 };
 
 template <int QH, int NW, bool TL>
-__global__ void __launch_bounds__(64 * NW, 1) ppo_act(ActArgs r) {
+__device__ __forceinline__ void act_body(ActArgs r) {
   constexpr int H = 64 * QH;
   constexpr int RPW = kRowTile / NW;
   constexpr int PH = lds_pitch(H), PA = lds_pitch(2 * H), PXMAX = lds_pitch(kMaxRowS);
@@ -1611,6 +1612,11 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_act(ActArgs r) {
   }
 }
 
+template <int QH, int NW, bool TL>
+__global__ void __launch_bounds__(64 * NW, 1) ppo_act(ActArgs r) {
+  act_body<QH, NW, TL>(r);
+}
+
 // ppo_act_c: ppo_act at H = 256 in the compact layout of ppo_rows_c -- the states / h1 / h2
 // images in two H-wide regions (P0 | P1: 71 KB with the head partials at 32-row tiles, 36 KB at
 // 16), [a1 | c1] kept in the layer-3 accumulators, <= 128 VGPRs: two workgroups per CU.
@@ -1619,8 +1625,7 @@ __global__ void __launch_bounds__(64 * NW, 1) ppo_act(ActArgs r) {
 // (A 4-deep ring with the one-workgroup-per-CU register budget at 4,096 rows measured 22.4 against
 // 21.9 us, round 5.)
 template <int QH, int NW, int RT>
-__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2 * NW / 4, 8)))
-ppo_act_c(ActArgs r) {
+__device__ __forceinline__ void act_c_body(ActArgs r) {
   constexpr int H = 64 * QH;
   constexpr int TW = H / NW / 16;
   constexpr int RB = RT / 16;
@@ -1708,6 +1713,12 @@ ppo_act_c(ActArgs r) {
   r.pre_tanh[2 * b + 1] = z1;
   r.logp[b] = lp;
   r.value[b] = val;
+}
+
+template <int QH, int NW, int RT>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2 * NW / 4, 8)))
+ppo_act_c(ActArgs r) {
+  act_c_body<QH, NW, RT>(r);
 }
 
 // ----------------------------------------------------------------------------- weight grads
@@ -2149,11 +2160,13 @@ __device__ __forceinline__ float wsum_item(const WgArgs& a, int item) {
 }
 
 // ppo_wsum: every work item of every weight-gradient tile, one sum-of-squares partial each
-__global__ void __launch_bounds__(256) ppo_wsum(WgArgs a) {
+__device__ __forceinline__ void wsum_body(const WgArgs& a) {
   __shared__ float red[4];
   const float tot = block_sum4(wsum_item(a, blockIdx.x), red);
   if (threadIdx.x == 0) a.norm_part[a.nh + blockIdx.x] = tot;
 }
+
+__global__ void __launch_bounds__(256) ppo_wsum(WgArgs a) { wsum_body(a); }
 
 // ----------------------------------------------------------------------------- reduce
 struct RedDesc {
@@ -2424,7 +2437,7 @@ __global__ void __launch_bounds__(256) ppo_adam(OptArgs o) {
 // (B = W) after a 4 x 4 transpose through LDS.  The small parameters (biases, heads, log_std)
 // follow in flat workgroups of 1,024.  Same Adam arithmetic per element as ppo_adam, so the same
 // bits; ppo_adam's one-element mapping scatters 4-byte image writes over 16 blocks per wave.
-__global__ void __launch_bounds__(256) ppo_adam_tiles(OptArgs o) {
+__device__ __forceinline__ void adam_tiles_body(const OptArgs& o) {
   __shared__ float red[4];
   __shared__ float sh[3];
   __shared__ __attribute__((aligned(16))) f32x4 tr[4][64];  // per wave: its block, [row][col]
@@ -2517,6 +2530,41 @@ __global__ void __launch_bounds__(256) ppo_adam_tiles(OptArgs o) {
   }
 }
 
+__global__ void __launch_bounds__(256) ppo_adam_tiles(OptArgs o) { adam_tiles_body(o); }
+
+// ----------------------------------------------------------------------------- grouped
+// G independent learners of the same dims in one launch per kernel (experiments/sweep.py: a
+// sweep's seeds of one condition).  Workgroup (x, y) runs the solo kernel's workgroup x for
+// learner y, whose arguments the kernel reads from a device table (hwy_ppo_group_prepare): the
+// same bodies and tile shapes as the solo launches, so each learner's bits are its solo run's.
+template <int QH, int NW, int RT>
+__global__ void __launch_bounds__(64 * NW, 1) ppo_rows_grp(const RowArgs* __restrict__ tab) {
+  rows_body<QH, NW, RT, false>(tab[blockIdx.y]);
+}
+
+__global__ void __launch_bounds__(512) ppo_wgrad_grp(const WgArgs* __restrict__ tab) {
+  ppo_wgrad_body(tab[blockIdx.y]);
+}
+
+__global__ void __launch_bounds__(256) ppo_wsum_grp(const WgArgs* __restrict__ tab) {
+  wsum_body(tab[blockIdx.y]);
+}
+
+__global__ void __launch_bounds__(256) ppo_adam_tiles_grp(const OptArgs* __restrict__ tab) {
+  adam_tiles_body(tab[blockIdx.y]);
+}
+
+template <int QH, int NW, bool TL>
+__global__ void __launch_bounds__(64 * NW, 1) ppo_act_grp(const ActArgs* __restrict__ tab) {
+  act_body<QH, NW, TL>(tab[blockIdx.y]);
+}
+
+template <int QH, int NW, int RT>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2 * NW / 4, 8)))
+ppo_act_c_grp(const ActArgs* __restrict__ tab) {
+  act_c_body<QH, NW, RT>(tab[blockIdx.y]);
+}
+
 template <int AM, int BM, int EPI>
 int launch_gemm(const GemmArgs& g, int splits, hipStream_t s) {
   dim3 grid((g.M + kTile - 1) / kTile, (g.N + kTile - 1) / kTile, splits);
@@ -2565,6 +2613,89 @@ int64_t hwy_ppo_tile_image_offset(const hwy_ppo_dims* d) {
   return (int64_t)(reinterpret_cast<char*>(w.wtile) - base);
 }
 
+// The fused path's per-kernel arguments for one learner's minibatch step (shared by the solo
+// launches and the grouped table of hwy_ppo_group_prepare).
+static RowArgs row_args(const hwy_ppo_args& a0, const Layout& L, const Work& w) {
+  const hwy_ppo_args* a = &a0;
+  const float* P = a->params;
+  const int B = a->dims.B, S = a->dims.S;
+  RowArgs r = {};
+  r.B = B, r.S = S;
+  r.states = a->states, r.idx = a->idx, r.pre_tanh = a->pre_tanh, r.old_logp = a->old_logp;
+  r.adv = a->adv, r.ret = a->ret, r.params = P;
+  for (int i = 0; i < 13; ++i) r.off[i] = L.off[i];
+  r.h1 = w.h1, r.h2 = w.h2, r.dac = w.dac, r.dh2 = w.dh2, r.dh1 = w.dh1, r.xg = w.xg;
+  r.tiles = w.wtile;
+  r.head_part = w.head_part, r.HP = w.HP;
+  r.eps_clip = a->eps_clip, r.value_coef = a->value_coef, r.entropy_coef = a->entropy_coef;
+  r.counters = a->counters;
+  return r;
+}
+
+static WgArgs wg_args(const hwy_ppo_args& a0, const Layout& L, const Work& w) {
+  const hwy_ppo_args* a = &a0;
+  const float* P = a->params;
+  const int B = a->dims.B, S = a->dims.S, H = a->dims.H;
+  WgArgs g = {};
+  g.B = B, g.S = S, g.H = H;
+  g.dac = w.dac, g.h2 = w.h2, g.dh2 = w.dh2, g.h1 = w.h1, g.dh1 = w.dh1, g.xg = w.xg;
+  g.grads = a->grads;
+  for (int i = 0; i < 13; ++i) g.off[i] = L.off[i];
+  g.head_part = w.head_part, g.nhp = w.n1, g.HP = w.HP, g.norm_part = w.norm_part;
+  g.tac = w.tac, g.t2 = w.t2, g.t1 = w.t1, g.nh = w.nh;
+  g.split = w.split, g.slab = w.wg_slab;
+  g.bal = w.bal, g.wm = w.wm, g.tpe = w.tpe, g.nslot = w.nslot;
+  g.entropy_coef = a->entropy_coef, g.value_coef = a->value_coef;
+  g.ent_const = 0.5f + 0.91893853320467274178f;
+  g.params = P, g.metrics = a->metrics, g.counters = a->counters;
+  return g;
+}
+
+// clip_grad_norm_ + Adam's arguments for one learner (solo launches and the grouped table)
+static OptArgs opt_args(const hwy_ppo_args& a0, const Layout& L, const Work& w) {
+  const hwy_ppo_args* a = &a0;
+  const hwy_ppo_dims& d = a->dims;
+  OptArgs o = {};
+  o.params = a->params, o.grads = a->grads, o.m = a->adam_m, o.v = a->adam_v;
+  // norm partials: ppo_sumsq / ppo_reduce write nred of them, ppo_wgrad grid2
+  o.norm_part = w.norm_part, o.numel = L.numel, o.counters = a->counters;
+  o.nred = (w.fused && !a->grads_modified) ? w.nred2 : w.nred;
+  o.lr = a->lr, o.beta1 = a->beta1, o.beta2 = a->beta2, o.eps = a->adam_eps;
+  o.max_norm = a->max_grad_norm;
+  if (w.fused) {
+    o.tiles = w.wtile;
+    o.o_w1 = L.off[P_W1], o.o_w2 = L.off[P_W2], o.o_wa1 = L.off[P_WA1], o.o_wc1 = L.off[P_WC1];
+    o.S = d.S, o.H = d.H, o.sb = w.sb, o.hb = w.hb;
+  }
+  o.skip = dev_knob_int("HWY_PPO_SKIP", 0) & 3;
+  if (w.fused) {  // ppo_adam_tiles' geometry (used when adam_tiles_ok)
+    const int kb1 = (d.S + 15) / 16;  // W1's live 16-column blocks
+    o.nkg1 = (kb1 + 3) / 4;
+    o.nwg1 = (d.H / 16) * o.nkg1;
+    o.nwgh = (d.H / 16) * (d.H / 64);
+    const int64_t r0[4] = {L.off[P_B1], L.off[P_B2], L.off[P_BA1], L.off[P_BC1]};
+    const int64_t r1[4] = {L.off[P_W2], L.off[P_WA1], L.off[P_WC1], L.numel};
+    o.run_pre[0] = 0;
+    for (int z = 0; z < 4; ++z) {
+      o.run_off[z] = r0[z];
+      o.run_pre[z + 1] = o.run_pre[z] + (r1[z] - r0[z]);
+    }
+  }
+  return o;
+}
+
+// the tile-major kernel wherever its float4s are aligned: S % 4 == 0 and 16-byte aligned bases
+static bool adam_tiles_ok(const hwy_ppo_args& a, const OptArgs& o, const Work& w) {
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
+  return w.fused && a.dims.S % 4 == 0 && al16(o.params) && al16(o.grads) && al16(o.m) &&
+         al16(o.v) && dev_knob_int("HWY_ADAM_FLAT", 0) == 0;
+}
+
+static int adam_tiles_grid(const OptArgs& o) {
+  const int nsmall = (int)((o.run_pre[4] + 1023) / 1024);
+  return o.nwg1 + 3 * o.nwgh + nsmall;
+}
+
 // mask (fused path; hwy_ppo_time_kernels launches them one at a time): bit 0 ppo_rows, bit 1
 // ppo_wgrad, bit 2 ppo_wsum
 static int forward_backward_k(const hwy_ppo_args* a, void* stream, int mask) {
@@ -2578,16 +2709,7 @@ static int forward_backward_k(const hwy_ppo_args* a, void* stream, int mask) {
   const float* P = a->params;
   int rc = 0;
   if (w.fused) {
-    RowArgs r = {};
-    r.B = B, r.S = S;
-    r.states = a->states, r.idx = a->idx, r.pre_tanh = a->pre_tanh, r.old_logp = a->old_logp;
-    r.adv = a->adv, r.ret = a->ret, r.params = P;
-    for (int i = 0; i < 13; ++i) r.off[i] = L.off[i];
-    r.h1 = w.h1, r.h2 = w.h2, r.dac = w.dac, r.dh2 = w.dh2, r.dh1 = w.dh1, r.xg = w.xg;
-    r.tiles = w.wtile;
-    r.head_part = w.head_part, r.HP = w.HP;
-    r.eps_clip = a->eps_clip, r.value_coef = a->value_coef, r.entropy_coef = a->entropy_coef;
-    r.counters = a->counters;
+    const RowArgs r = row_args(*a, L, w);
     // 8 waves (2 per SIMD) when the columns split into 16-wide tiles, else 4
     const dim3 g1(w.n1), b4(256), b8(512), blk(256);
     if (!(mask & 1)) {
@@ -2617,18 +2739,7 @@ static int forward_backward_k(const hwy_ppo_args* a, void* stream, int mask) {
       }
     }
     rc |= hipGetLastError() == hipSuccess ? 0 : -1;
-    WgArgs g = {};
-    g.B = B, g.S = S, g.H = H;
-    g.dac = w.dac, g.h2 = w.h2, g.dh2 = w.dh2, g.h1 = w.h1, g.dh1 = w.dh1, g.xg = w.xg;
-    g.grads = a->grads;
-    for (int i = 0; i < 13; ++i) g.off[i] = L.off[i];
-    g.head_part = w.head_part, g.nhp = w.n1, g.HP = w.HP, g.norm_part = w.norm_part;
-    g.tac = w.tac, g.t2 = w.t2, g.t1 = w.t1, g.nh = w.nh;
-    g.split = w.split, g.slab = w.wg_slab;
-    g.bal = w.bal, g.wm = w.wm, g.tpe = w.tpe, g.nslot = w.nslot;
-    g.entropy_coef = a->entropy_coef, g.value_coef = a->value_coef;
-    g.ent_const = 0.5f + 0.91893853320467274178f;
-    g.params = P, g.metrics = a->metrics, g.counters = a->counters;
+    const WgArgs g = wg_args(*a, L, w);
     if (mask & 2) hipLaunchKernelGGL(ppo_wgrad, dim3(w.grid2), dim3(64 * kWgWaves), 0, s, g);
     rc |= hipGetLastError() == hipSuccess ? 0 : -1;
     if (mask & 4)
@@ -2768,36 +2879,9 @@ int hwy_ppo_optimizer(const hwy_ppo_args* a, void* stream) {
                        w.norm_part);
     if (hipGetLastError() != hipSuccess) return -1;
   }
-  OptArgs o = {};
-  o.params = a->params, o.grads = a->grads, o.m = a->adam_m, o.v = a->adam_v;
-  // norm partials: ppo_sumsq / ppo_reduce write nred of them, ppo_wgrad grid2
-  o.norm_part = w.norm_part, o.numel = L.numel, o.counters = a->counters;
-  o.nred = (w.fused && !a->grads_modified) ? w.nred2 : w.nred;
-  o.lr = a->lr, o.beta1 = a->beta1, o.beta2 = a->beta2, o.eps = a->adam_eps;
-  o.max_norm = a->max_grad_norm;
-  if (w.fused) {
-    o.tiles = w.wtile;
-    o.o_w1 = L.off[P_W1], o.o_w2 = L.off[P_W2], o.o_wa1 = L.off[P_WA1], o.o_wc1 = L.off[P_WC1];
-    o.S = d.S, o.H = d.H, o.sb = w.sb, o.hb = w.hb;
-  }
-  o.skip = dev_knob_int("HWY_PPO_SKIP", 0) & 3;
-  // the tile-major kernel wherever its float4s are aligned: S % 4 == 0 and 16-byte aligned bases
-  auto al16 = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
-  if (w.fused && d.S % 4 == 0 && al16(o.params) && al16(o.grads) && al16(o.m) && al16(o.v) &&
-      dev_knob_int("HWY_ADAM_FLAT", 0) == 0) {
-    const int kb1 = (d.S + 15) / 16;  // W1's live 16-column blocks
-    o.nkg1 = (kb1 + 3) / 4;
-    o.nwg1 = (d.H / 16) * o.nkg1;
-    o.nwgh = (d.H / 16) * (d.H / 64);
-    const int64_t r0[4] = {L.off[P_B1], L.off[P_B2], L.off[P_BA1], L.off[P_BC1]};
-    const int64_t r1[4] = {L.off[P_W2], L.off[P_WA1], L.off[P_WC1], L.numel};
-    o.run_pre[0] = 0;
-    for (int z = 0; z < 4; ++z) {
-      o.run_off[z] = r0[z];
-      o.run_pre[z + 1] = o.run_pre[z] + (r1[z] - r0[z]);
-    }
-    const int nsmall = (int)((o.run_pre[4] + 1023) / 1024);
-    hipLaunchKernelGGL(ppo_adam_tiles, dim3(o.nwg1 + 3 * o.nwgh + nsmall), dim3(256), 0, s, o);
+  OptArgs o = opt_args(*a, L, w);
+  if (adam_tiles_ok(*a, o, w)) {
+    hipLaunchKernelGGL(ppo_adam_tiles, dim3(adam_tiles_grid(o)), dim3(256), 0, s, o);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
   const int nadam = (int)((L.numel + 256 * kAdamEPT - 1) / (256 * kAdamEPT));
@@ -2924,6 +3008,161 @@ int hwy_ppo_act(const hwy_ppo_act_args* a, void* stream) {
     else
       hipLaunchKernelGGL((ppo_act_c<4, 8, 16>), dim3((d.B + 15) / 16), b8, 0, s, r);
   } else if (r.tiles)
+    launch(std::integral_constant<bool, true>());
+  else
+    launch(std::integral_constant<bool, false>());
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---- grouped learners (include/hwy_ppo.h): the device table of one minibatch step is
+// [G RowArgs | G WgArgs | G OptArgs], each section 256-byte aligned
+static int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
+static int64_t grp_row_off(int) { return 0; }
+static int64_t grp_wg_off(int G) { return align256((int64_t)G * sizeof(RowArgs)); }
+static int64_t grp_opt_off(int G) { return grp_wg_off(G) + align256((int64_t)G * sizeof(WgArgs)); }
+
+static bool group_dims_ok(const hwy_ppo_dims& d) {
+  if (hwy_ppo_workspace_bytes(&d) < 0 || !fused_ok(d) || d.A != 2 || d.B < 1) return false;
+  char* base = reinterpret_cast<char*>(uintptr_t(1) << 20);  // carve only adds offsets to it
+  const Work w = carve(d, base, nullptr);
+  return w.fused && w.rt == kRowTile;  // 16-row tiles: minibatches below the 32-row threshold
+}
+
+int64_t hwy_ppo_group_table_bytes(const hwy_ppo_dims* d, int G) {
+  if (!d || G < 1 || !group_dims_ok(*d)) return -1;
+  return grp_opt_off(G) + align256((int64_t)G * sizeof(OptArgs));
+}
+
+int hwy_ppo_group_prepare(const hwy_ppo_args* a, int G, void* table, void* stream) {
+  if (!a || G < 1 || !table) return -1;
+  const hwy_ppo_dims& d = a[0].dims;
+  if (!group_dims_ok(d)) return -1;
+  const Layout L = make_layout(d);
+  const int64_t bytes = hwy_ppo_group_table_bytes(&d, G);
+  char* host = static_cast<char*>(calloc((size_t)bytes, 1));
+  if (!host) return -2;
+  int rc = 0;
+  for (int g = 0; g < G && rc == 0; ++g) {
+    const hwy_ppo_args& ag = a[g];
+    if (memcmp(&ag.dims, &d, sizeof(d)) != 0 || ag.grads_modified || !ag.workspace ||
+        !ag.counters || !ag.params || !ag.grads || !ag.adam_m || !ag.adam_v) {
+      rc = -1;
+      break;
+    }
+    const Work w = carve(d, ag.workspace, nullptr);
+    const OptArgs o = opt_args(ag, L, w);
+    if (!adam_tiles_ok(ag, o, w)) {
+      rc = -1;
+      break;
+    }
+    reinterpret_cast<RowArgs*>(host + grp_row_off(G))[g] = row_args(ag, L, w);
+    reinterpret_cast<WgArgs*>(host + grp_wg_off(G))[g] = wg_args(ag, L, w);
+    reinterpret_cast<OptArgs*>(host + grp_opt_off(G))[g] = o;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (rc == 0 && (hipMemcpyAsync(table, host, (size_t)bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+                  hipStreamSynchronize(s) != hipSuccess))
+    rc = -2;
+  free(host);
+  return rc;
+}
+
+int hwy_ppo_group_step(const hwy_ppo_dims* d, int G, const void* table, void* stream) {
+  if (!d || G < 1 || !table || !group_dims_ok(*d)) return -1;
+  char* base = reinterpret_cast<char*>(uintptr_t(1) << 20);
+  const Work w = carve(*d, base, nullptr);
+  const Layout L = make_layout(*d);
+  hwy_ppo_args geom = {};
+  geom.dims = *d;
+  const OptArgs og = opt_args(geom, L, w);  // the grid geometry only
+  const char* t = static_cast<const char*>(table);
+  const RowArgs* tr = reinterpret_cast<const RowArgs*>(t + grp_row_off(G));
+  const WgArgs* tw = reinterpret_cast<const WgArgs*>(t + grp_wg_off(G));
+  const OptArgs* to = reinterpret_cast<const OptArgs*>(t + grp_opt_off(G));
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g1(w.n1, G), b4(256), b8(512);
+  switch (d->H / 64) {
+    case 1: hipLaunchKernelGGL((ppo_rows_grp<1, 4, 16>), g1, b4, 0, s, tr); break;
+    case 2: hipLaunchKernelGGL((ppo_rows_grp<2, 8, 16>), g1, b8, 0, s, tr); break;
+    case 3: hipLaunchKernelGGL((ppo_rows_grp<3, 4, 16>), g1, b4, 0, s, tr); break;
+    case 4: hipLaunchKernelGGL((ppo_rows_grp<4, 8, 16>), g1, b8, 0, s, tr); break;
+    case 5: hipLaunchKernelGGL((ppo_rows_grp<5, 4, 16>), g1, b4, 0, s, tr); break;
+    case 6: hipLaunchKernelGGL((ppo_rows_grp<6, 8, 16>), g1, b8, 0, s, tr); break;
+    case 7: hipLaunchKernelGGL((ppo_rows_grp<7, 4, 16>), g1, b4, 0, s, tr); break;
+    default: hipLaunchKernelGGL((ppo_rows_grp<8, 8, 16>), g1, b8, 0, s, tr); break;
+  }
+  int rc = hipGetLastError() == hipSuccess ? 0 : -1;
+  hipLaunchKernelGGL(ppo_wgrad_grp, dim3(w.grid2, G), dim3(64 * kWgWaves), 0, s, tw);
+  rc |= hipGetLastError() == hipSuccess ? 0 : -1;
+  hipLaunchKernelGGL(ppo_wsum_grp, dim3((w.tac + w.t2 + w.t1) * (kWgTM * kWgTN / 1024), G),
+                     dim3(256), 0, s, tw);
+  rc |= hipGetLastError() == hipSuccess ? 0 : -1;
+  hipLaunchKernelGGL(ppo_adam_tiles_grp, dim3(adam_tiles_grid(og), G), dim3(256), 0, s, to);
+  rc |= hipGetLastError() == hipSuccess ? 0 : -1;
+  return rc;
+}
+
+int64_t hwy_ppo_group_act_table_bytes(int G) {
+  return G < 1 ? -1 : align256((int64_t)G * sizeof(ActArgs));
+}
+
+int hwy_ppo_group_act_prepare(const hwy_ppo_act_args* a, int G, void* table, void* stream) {
+  if (!a || G < 1 || !table) return -1;
+  const hwy_ppo_dims& d = a[0].dims;
+  if (!fused_ok(d) || d.A != 2 || d.B < 1) return -1;
+  const Layout L = make_layout(d);
+  const int64_t bytes = hwy_ppo_group_act_table_bytes(G);
+  char* host = static_cast<char*>(calloc((size_t)bytes, 1));
+  if (!host) return -2;
+  int rc = 0;
+  for (int g = 0; g < G; ++g) {
+    const hwy_ppo_act_args& ag = a[g];
+    if (memcmp(&ag.dims, &d, sizeof(d)) != 0 || !ag.states || !ag.params || !ag.action ||
+        !ag.pre_tanh || !ag.logp || !ag.value || (!ag.tiles) != (!a[0].tiles) ||
+        (!ag.noise) != (!a[0].noise)) {
+      rc = -1;
+      break;
+    }
+    ActArgs r = {};
+    r.B = d.B, r.S = d.S, r.states = ag.states, r.params = ag.params, r.noise = ag.noise;
+    for (int i = 0; i < 13; ++i) r.off[i] = L.off[i];
+    r.action = ag.action, r.pre_tanh = ag.pre_tanh, r.logp = ag.logp, r.value = ag.value;
+    r.tiles = ag.tiles;
+    reinterpret_cast<ActArgs*>(host)[g] = r;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (rc == 0 && (hipMemcpyAsync(table, host, (size_t)bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+                  hipStreamSynchronize(s) != hipSuccess))
+    rc = -2;
+  free(host);
+  return rc;
+}
+
+int hwy_ppo_group_act(const hwy_ppo_dims* d, int G, int tiles, const void* table, void* stream) {
+  if (!d || G < 1 || !table || !fused_ok(*d) || d->A != 2 || d->B < 1) return -1;
+  const ActArgs* ta = static_cast<const ActArgs*>(table);
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g((d->B + kRowTile - 1) / kRowTile, G), b4(256), b8(512);
+  auto launch = [&](auto tl) {
+    constexpr bool TL = decltype(tl)::value;
+    switch (d->H / 64) {
+      case 1: hipLaunchKernelGGL((ppo_act_grp<1, 4, TL>), g, b4, 0, s, ta); break;
+      case 2: hipLaunchKernelGGL((ppo_act_grp<2, 8, TL>), g, b8, 0, s, ta); break;
+      case 3: hipLaunchKernelGGL((ppo_act_grp<3, 4, TL>), g, b4, 0, s, ta); break;
+      case 4: hipLaunchKernelGGL((ppo_act_grp<4, 8, TL>), g, b8, 0, s, ta); break;
+      case 5: hipLaunchKernelGGL((ppo_act_grp<5, 4, TL>), g, b4, 0, s, ta); break;
+      case 6: hipLaunchKernelGGL((ppo_act_grp<6, 8, TL>), g, b8, 0, s, ta); break;
+      case 7: hipLaunchKernelGGL((ppo_act_grp<7, 4, TL>), g, b4, 0, s, ta); break;
+      default: hipLaunchKernelGGL((ppo_act_grp<8, 8, TL>), g, b8, 0, s, ta); break;
+    }
+  };
+  // the solo hwy_ppo_act's kernel choice, per learner's B (so each learner's bits are its solo's)
+  if (tiles && d->H == 256) {
+    if (d->B >= 64 * chip_geom().cus)
+      hipLaunchKernelGGL((ppo_act_c_grp<4, 8, 32>), dim3((d->B + 31) / 32, G), b8, 0, s, ta);
+    else
+      hipLaunchKernelGGL((ppo_act_c_grp<4, 8, 16>), dim3((d->B + 15) / 16, G), b8, 0, s, ta);
+  } else if (tiles)
     launch(std::integral_constant<bool, true>());
   else
     launch(std::integral_constant<bool, false>());

@@ -68,7 +68,9 @@ def lib():
     L.hwy_obs_pe.argtypes = [vp, vp, i32, i32, i32, i32, i32, i32, f32, vp, vp, vp]
     L.hwy_gae.argtypes = [vp, vp, vp, vp, f64, f64, i32, i32, vp, vp, vp]
     L.hwy_math_selftest.argtypes = [i32, vp, vp, vp, i32, vp]
-    for name in ("hwy_create", "hwy_obs_features", "hwy_set_pe_table", "hwy_set_seed_schedule", "hwy_reset", "hwy_step",
+    L.hwy_set_seed_groups.argtypes = [vp, vp, i32, i32]
+    for name in ("hwy_create", "hwy_obs_features", "hwy_set_pe_table", "hwy_set_seed_schedule",
+                 "hwy_set_seed_groups", "hwy_reset", "hwy_step",
                  "hwy_export_state", "hwy_import_state", "hwy_obs_pe", "hwy_gae",
                  "hwy_math_selftest"):
         getattr(L, name).restype = i32

@@ -75,6 +75,23 @@ def _bind(L):
     L.hwy_ppo_time_kernels.restype = ctypes.c_int
     L.hwy_ppo_tile_image_offset.argtypes = [ctypes.POINTER(PpoDims)]
     L.hwy_ppo_tile_image_offset.restype = ctypes.c_int64
+    # grouped learners (include/hwy_ppo.h)
+    L.hwy_ppo_group_table_bytes.argtypes = [ctypes.POINTER(PpoDims), ctypes.c_int]
+    L.hwy_ppo_group_table_bytes.restype = ctypes.c_int64
+    L.hwy_ppo_group_prepare.argtypes = [ctypes.POINTER(PpoArgs), ctypes.c_int, ctypes.c_void_p,
+                                        ctypes.c_void_p]
+    L.hwy_ppo_group_prepare.restype = ctypes.c_int
+    L.hwy_ppo_group_step.argtypes = [ctypes.POINTER(PpoDims), ctypes.c_int, ctypes.c_void_p,
+                                     ctypes.c_void_p]
+    L.hwy_ppo_group_step.restype = ctypes.c_int
+    L.hwy_ppo_group_act_table_bytes.argtypes = [ctypes.c_int]
+    L.hwy_ppo_group_act_table_bytes.restype = ctypes.c_int64
+    L.hwy_ppo_group_act_prepare.argtypes = [ctypes.POINTER(PpoActArgs), ctypes.c_int,
+                                            ctypes.c_void_p, ctypes.c_void_p]
+    L.hwy_ppo_group_act_prepare.restype = ctypes.c_int
+    L.hwy_ppo_group_act.argtypes = [ctypes.POINTER(PpoDims), ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_void_p, ctypes.c_void_p]
+    L.hwy_ppo_group_act.restype = ctypes.c_int
     L._ppo_bound = True
     return L
 
@@ -187,6 +204,16 @@ def act_supported(S: int, H: int, A: int) -> bool:
     return A == 2 and S % 4 == 0 and S <= 256 and H % 64 == 0 and 64 <= H <= 512
 
 
+def act_tiles(agent, flat: torch.Tensor, S: int, H: int) -> Optional[int]:
+    """The weight tile image fused_act streams for this agent (None: the params rows): its
+    FusedPPO's when in step, else at H = 256 an acting-only image (_act_tiles)."""
+    F = getattr(agent, "_fused", None)
+    t = F.current_tiles(flat) if F is not None else None
+    if t is None and H == _ACT_C_HIDDEN:
+        t = _act_tiles(agent, flat, S, H)
+    return t
+
+
 def fused_act(agent, states: torch.Tensor, deterministic: bool = False,
               generator: Optional[torch.Generator] = None, out=None,
               noise: Optional[torch.Tensor] = None):
@@ -225,10 +252,7 @@ def fused_act(agent, states: torch.Tensor, deterministic: bool = False,
     a.noise = None if noise is None else noise.data_ptr()
     a.action, a.pre_tanh, a.logp, a.value = (action.data_ptr(), pre.data_ptr(), logp.data_ptr(),
                                              value.data_ptr())
-    F = getattr(agent, "_fused", None)
-    a.tiles = F.current_tiles(flat) if F is not None else None
-    if a.tiles is None and H == _ACT_C_HIDDEN:
-        a.tiles = _act_tiles(agent, flat, S, H)
+    a.tiles = act_tiles(agent, flat, S, H)
     check(_bind(lib()).hwy_ppo_act(ctypes.byref(a), stream_ptr()), "hwy_ppo_act")
     return action, pre, logp, value
 
@@ -531,3 +555,105 @@ class FusedPPO:
         self._graphs = [g]
         self._captured_collectives = True
         return True
+
+
+# ------------------------------------------------------------------ grouped learners
+class GroupAct:
+    """ActorCritic.act for G agents of the same dims in ONE launch (hwy_ppo_group_act): agent g
+    acts on rows [g*B, (g+1)*B) of `states` and writes the same rows of the outputs, each
+    bit for bit what fused_act(agent g, its rows) writes.  The kernel arguments live in a device
+    table prepared once per (buffers, weights) key, so the launch is graph-capturable."""
+
+    def __init__(self, agents, B: int):
+        self.agents = list(agents)
+        self.G, self.B = len(self.agents), int(B)
+        self.L = _bind(lib())
+        ac = self.agents[0].actor_critic
+        self.S = ac.shared[0].weight.shape[1]
+        self.H = ac.shared[0].weight.shape[0]
+        self.dims = PpoDims(self.B, self.S, self.H, 2)
+        nb = self.L.hwy_ppo_group_act_table_bytes(self.G)
+        self.dev = self.agents[0].device
+        self._tables = {}
+        self._nb = int(nb)
+
+    def tiles(self):
+        out = []
+        for ag in self.agents:
+            flat = flat_params(ag)[0]
+            out.append(act_tiles(ag, flat, self.S, self.H))
+        return out
+
+    def table(self, states, noise, out, tiles) -> torch.Tensor:
+        """The device argument table for these buffers (cached by their addresses)."""
+        action, pre, logp, value = out
+        key = (states.data_ptr(), None if noise is None else noise.data_ptr(),
+               action.data_ptr(), pre.data_ptr(), logp.data_ptr(), value.data_ptr(), tuple(tiles),
+               tuple(flat_params(ag)[0].data_ptr() for ag in self.agents))
+        t = self._tables.get(key)
+        if t is not None:
+            return t
+        B = self.B
+        arr = (PpoActArgs * self.G)()
+        for g, (ag, tl) in enumerate(zip(self.agents, tiles)):
+            a = arr[g]
+            a.dims = self.dims
+            a.states = states.data_ptr() + g * B * self.S * 4
+            a.params = flat_params(ag)[0].data_ptr()
+            a.noise = None if noise is None else noise.data_ptr() + g * B * 2 * 4
+            a.action = action.data_ptr() + g * B * 2 * 4
+            a.pre_tanh = pre.data_ptr() + g * B * 2 * 4
+            a.logp = logp.data_ptr() + g * B * 4
+            a.value = value.data_ptr() + g * B * 4
+            a.tiles = tl
+        t = torch.empty(self._nb, dtype=torch.uint8, device=self.dev)
+        check(self.L.hwy_ppo_group_act_prepare(arr, self.G, t.data_ptr(), stream_ptr()),
+              "hwy_ppo_group_act_prepare")
+        self._tables[key] = t
+        return t
+
+    def __call__(self, states, out, noise=None, tiles=None):
+        """states [G*B, S]; out = (action [G*B,2], pre_tanh [G*B,2], logp [G*B], value [G*B]);
+        noise [G*B, 2] or None (deterministic)."""
+        tiles = self.tiles() if tiles is None else tiles
+        t = self.table(states, noise, out, tiles)
+        check(self.L.hwy_ppo_group_act(ctypes.byref(self.dims), self.G,
+                                       int(tiles[0] is not None), t.data_ptr(), stream_ptr()),
+              "hwy_ppo_group_act")
+
+
+class GroupStep:
+    """One minibatch step of G FusedPPO learners (same dims) in four launches
+    (hwy_ppo_group_step): learner g's arguments are its own FusedPPO._args, so each learner
+    steps bit for bit as its solo run() would.  One device table per minibatch index."""
+
+    def __init__(self, fused):
+        self.fused = list(fused)
+        self.G = len(self.fused)
+        F0 = self.fused[0]
+        self.L = F0.L
+        self.dims = F0.dims
+        nb = self.L.hwy_ppo_group_table_bytes(ctypes.byref(self.dims), self.G)
+        if nb < 0:
+            raise ValueError(f"grouped PPO step: unsupported dims B={F0.mb} S={F0.S} H={F0.H} "
+                             "(16-row tiles: minibatches below 8,192 rows)")
+        self._nb = int(nb)
+        self.tables: List[torch.Tensor] = []
+
+    def prepare(self, per_learner_args) -> None:
+        """per_learner_args[g][i]: learner g's PpoArgs of minibatch i."""
+        nmb = len(per_learner_args[0])
+        self.tables = []
+        for i in range(nmb):
+            arr = (PpoArgs * self.G)()
+            for g in range(self.G):
+                ctypes.memmove(ctypes.byref(arr[g]), ctypes.byref(per_learner_args[g][i]),
+                               ctypes.sizeof(PpoArgs))
+            t = torch.empty(self._nb, dtype=torch.uint8, device=self.fused[0].flat.device)
+            check(self.L.hwy_ppo_group_prepare(arr, self.G, t.data_ptr(), stream_ptr()),
+                  "hwy_ppo_group_prepare")
+            self.tables.append(t)
+
+    def step(self, i: int) -> None:
+        check(self.L.hwy_ppo_group_step(ctypes.byref(self.dims), self.G, self.tables[i].data_ptr(),
+                                        stream_ptr()), "hwy_ppo_group_step")

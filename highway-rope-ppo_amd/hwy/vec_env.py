@@ -200,6 +200,26 @@ class HighwayVecEnv:
               "hwy_set_seed_schedule")
         self.launch_version += 1
 
+    def set_seed_groups(self, seed_bases, envs_per_group: int) -> None:
+        """Split the E envs into experiment groups of ``envs_per_group`` consecutive envs, group
+        g seeded as a solo handle of that many envs with ``set_seed_schedule(seed_bases[g])``
+        would be: seed(env l of group g, episode k) = seed_bases[g] + l + 1 + envs_per_group*k
+        (hwy_set_seed_groups; experiments/sweep.py).  ``seed_bases=None`` turns grouping off."""
+        if seed_bases is None:
+            check(lib().hwy_set_seed_groups(self._handle, None, 0, 1), "hwy_set_seed_groups")
+            self._groups = None
+        else:
+            b = np.ascontiguousarray(np.asarray(seed_bases, dtype=np.int64))
+            check(lib().hwy_set_seed_groups(self._handle, b.ctypes.data_as(ctypes.c_void_p),
+                                            int(b.size), int(envs_per_group)),
+                  "hwy_set_seed_groups")
+            c = self._cfg
+            c.seed_stride = int(envs_per_group)
+            check(lib().hwy_set_seed_schedule(self._handle, c.seed_base, c.env_offset,
+                                              c.seed_stride), "hwy_set_seed_schedule")
+            self._groups = (b.copy(), int(envs_per_group))
+        self.launch_version += 1
+
     def export_state(self) -> torch.Tensor:
         out = torch.empty(NFIELDS, self.num_envs, HWY_MAX_VEHICLES, dtype=torch.int32,
                           device=self.device)

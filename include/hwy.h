@@ -164,13 +164,24 @@ void hwy_destroy(hwy_handle* h);
 int hwy_obs_features(const hwy_handle* h);
 
 /* Host table for the fused wrapper: rank -> tanh(W) [N*d]; dist -> freqs [d/2];
- * rope -> inv_freq [rotate_dim/2]. Synchronous (setup time only). */
+ * rope -> inv_freq [rotate_dim/2]; with experiment groups (hwy_set_seed_groups) also
+ * n_groups RankPE tables [n_groups*N*d], one per group. Synchronous (setup time only). */
 int hwy_set_pe_table(hwy_handle* h, const float* table_host, int n);
 
 /* Change the episode seed schedule (seed_base, env_offset, seed_stride) of an existing handle:
  * training/routine.py re-seeds every episode from exp_seed (routine.py:127) and every evaluation
  * from exp_seed + 1000 (routine.py:18).  Takes effect for the next reset / autoreset. */
 int hwy_set_seed_schedule(hwy_handle* h, int64_t seed_base, int32_t env_offset, int64_t seed_stride);
+
+/* Experiment groups (a sweep's seeds batched into one handle; experiments/sweep.py): the E envs
+ * form E / envs_per_group groups of consecutive envs, group g an experiment of its own with
+ * seed(env g*envs_per_group + l, episode k) = seed_bases[g] + env_offset + l + 1 + seed_stride*k
+ * (set seed_stride = envs_per_group for the solo schedule of each group: the same seeds, so each
+ * group's envs step bit for bit as a solo handle of envs_per_group envs would).  seed_bases
+ * (host, [E / envs_per_group]) is copied; n_groups = 0 turns grouping off.  With a fused RankPE,
+ * hwy_set_pe_table may then take n_groups tables back to back (group g reads table g).
+ * Synchronous (setup time only). */
+int hwy_set_seed_groups(hwy_handle* h, const int64_t* seed_bases, int n_groups, int envs_per_group);
 
 /* Reset envs whose mask byte is nonzero (mask NULL = all) with the given per-env seeds
  * (seeds NULL = the autoreset schedule with k = 0). Writes obs [E, N, F_out] for reset envs. */

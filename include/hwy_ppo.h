@@ -109,6 +109,27 @@ typedef struct hwy_ppo_act_args {
 } hwy_ppo_act_args;
 int hwy_ppo_act(const hwy_ppo_act_args* a, void* stream);
 
+/* ---- Grouped learners: G independent learners of the same dims (a sweep's seeds of one
+ * condition, experiments/sweep.py; the reference runs them as separate processes,
+ * experiments/runner.py:46-155 under main.py:188-242's joblib / SLURM fan-out) stepped in ONE
+ * launch per kernel.  Workgroup (x, y) runs the solo launch's workgroup x for learner y, whose
+ * kernel arguments the kernels read from a device table; the kernel bodies and tile shapes are
+ * the solo calls', so each learner's results are bit for bit its solo run's.  The *_prepare
+ * calls build a table from G argument structs (synchronous: they wait for `stream`; not
+ * capturable); the launch calls are asynchronous and hipGraph-capturable.
+ *
+ * hwy_ppo_group_step = hwy_ppo_forward_backward + hwy_ppo_optimizer for every learner (fused
+ * path with 16-row tiles, i.e. minibatches below 64 x CUs rows; grads_modified == 0; 16-byte
+ * aligned flat buffers).  -1 bad arguments / unsupported dims, -2 HIP error. */
+int64_t hwy_ppo_group_table_bytes(const hwy_ppo_dims* d, int G);
+int hwy_ppo_group_prepare(const hwy_ppo_args* a /*[G]*/, int G, void* table, void* stream);
+int hwy_ppo_group_step(const hwy_ppo_dims* d, int G, const void* table, void* stream);
+/* hwy_ppo_act for G learners; `tiles` = whether the learners' args carry tile images (all or
+ * none), which picks the solo call's kernel. */
+int64_t hwy_ppo_group_act_table_bytes(int G);
+int hwy_ppo_group_act_prepare(const hwy_ppo_act_args* a /*[G]*/, int G, void* table, void* stream);
+int hwy_ppo_group_act(const hwy_ppo_dims* d, int G, int tiles, const void* table, void* stream);
+
 /* Build flags of this library: bit 0 = development knobs compiled in (HWY_DEV_KNOBS: the
  * HWY_WG_BAL / HWY_ROWS_RT / HWY_WG_FILL environment variables are read), bit 1 = section clocks
  * (HWY_SECTION_PROFILE).  A product build returns 0 and reads no environment variable. */

@@ -144,3 +144,24 @@ def test_kernel_sources_carry_no_ab_knob_forest():
     assert n <= 3
     dev = open(os.path.join(csrc, "hwy_dev_knobs.h")).read()
     assert "HWY_SKIP" in dev
+
+
+def test_group_table_geometry_without_gpu(lib):
+    """hwy_ppo_group_table_bytes (include/hwy_ppo.h): the grouped step covers the fused path's
+    16-row tiles (a sweep experiment's 64-row minibatches), not the 32- / 64-row tiles of large
+    minibatches; the table grows with the learner count."""
+    from hwy.ppo_native import PpoDims
+
+    f = lib.hwy_ppo_group_table_bytes
+    f.restype = ctypes.c_int64
+    f.argtypes = [ctypes.POINTER(PpoDims), ctypes.c_int]
+    one = f(ctypes.byref(PpoDims(64, 60, 256, 2)), 1)
+    ten = f(ctypes.byref(PpoDims(64, 60, 256, 2)), 10)
+    assert 0 < one < ten and ten % 256 == 0
+    assert f(ctypes.byref(PpoDims(64, 120, 512, 2)), 10) > 0
+    assert f(ctypes.byref(PpoDims(16384, 60, 256, 2)), 10) == -1  # 32-row tiles
+    assert f(ctypes.byref(PpoDims(64, 62, 256, 2)), 10) == -1     # S % 4 != 0: general path
+    assert f(ctypes.byref(PpoDims(64, 60, 256, 2)), 0) == -1
+    g = lib.hwy_ppo_group_act_table_bytes
+    g.restype = ctypes.c_int64
+    assert g(10) > g(1) > 0 and g(0) == -1

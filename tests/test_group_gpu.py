@@ -1,0 +1,109 @@
+"""ExperimentGroup (ppo/group.py): G experiments of one condition batched into the launches
+themselves (grouped env handle, grouped acting, grouped minibatch steps) must each be bit for
+bit their solo run -- the runner's construction (experiments/runner.py:102-138) and
+training/routine.py's _train_vector loop (LockstepRollout + update_rollout) with the same seed.
+Checked on every rollout row, the final weights, Adam moments and the metrics."""
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _hp(H, epochs=2):
+    return dict(lr=3e-4, epochs=epochs, batch_size=64, hidden_dim=H)
+
+
+def _solo(cond, d, seed, E, T, iters, H, overrides):
+    from config.base_config import HIGHWAY_CONFIG
+    from experiments.wrappers import make_env
+    from ppo.agent import PPOAgent, RolloutBuffer
+    from ppo.rollout import LockstepRollout
+    from utils.reproducibility import set_random_seeds
+
+    set_random_seeds(seed)
+    env = make_env(cond, HIGHWAY_CONFIG, d_embed=d,
+                   env_overrides=dict(overrides, num_envs=E, device=DEV, autoreset=True))
+    if hasattr(env, "to"):
+        env = env.to(DEV)
+    base = env.unwrapped
+    sd = base.obs_rows * base.obs_features
+    agent = PPOAgent(sd, 2, device=DEV, **_hp(H))
+    base.set_seed_schedule(seed)
+    obs, _ = env.reset()
+    buf = RolloutBuffer(T, E, sd, 2, DEV)
+    buf.states[0].copy_(obs.reshape(E, sd))
+    roll = LockstepRollout(agent, base, buf)
+    hist, metrics = [], []
+    for _ in range(iters):
+        roll.run()
+        hist.append({k: getattr(buf, k).clone() for k in ("states", "actions", "rewards", "dones",
+                                                          "log_probs", "values")})
+        metrics.append(agent.update_rollout(buf, agent.value(buf.states[T])))
+        buf.states[0].copy_(buf.states[T])
+    torch.cuda.synchronize()
+    return agent, hist, metrics, env
+
+
+@pytest.mark.parametrize("cond_name,d,H,order", [("SORTED", None, 256, None),
+                                                 ("SHUFFLED_RANKPE", 4, 384, "shuffled"),
+                                                 ("SHUFFLED_ROPE", 4, 256, "shuffled")])
+def test_group_matches_solo_runs_bit_for_bit(cond_name, d, H, order):
+    from config.base_config import HIGHWAY_CONFIG
+    from experiments.config import Condition
+    from ppo.group import build_group
+
+    cond = Condition[cond_name]
+    seeds, E, T, iters = [42, 1042, 2042], 16, 16, 3
+    overrides = {} if order is None else {"observation": {"order": order}}
+    grp = build_group(cond, HIGHWAY_CONFIG, _hp(H), seeds, E, T, DEV, d_embed=d,
+                      env_overrides=overrides)
+    ghist, gmet = [], []
+    for _ in range(iters):
+        grp.rollout()
+        b = grp.buf
+        ghist.append({k: getattr(b, k).clone() for k in ("states", "actions", "rewards", "dones",
+                                                         "log_probs", "values")})
+        gmet.append(grp.update())
+    torch.cuda.synchronize()
+    assert grp.agents[0]._fused is not None and grp.agents[0]._fused.mb == 64
+    for g, s in enumerate(seeds):
+        agent, hist, metrics, env = _solo(cond, d, s, E, T, iters, H, overrides)
+        sl = slice(g * E, (g + 1) * E)
+        for it in range(iters):
+            for k, v in hist[it].items():
+                assert torch.equal(ghist[it][k][:, sl], v), (g, it, k)
+            assert gmet[it][g] == metrics[it], (g, it)
+        for (k, va), (_, vb) in zip(agent.actor_critic.state_dict().items(),
+                                    grp.agents[g].actor_critic.state_dict().items()):
+            assert torch.equal(va, vb), (g, k)
+        Fs, Fg = agent._fused, grp.agents[g]._fused
+        assert torch.equal(Fs.m, Fg.m) and torch.equal(Fs.v, Fg.v), g
+        assert int(Fs.counters[0]) == int(Fg.counters[0]) == iters * 2 * (T * E // 64)
+        env.close()
+    # the episodes of each experiment come out of its own slice
+    assert grp.episode_returns(0).numel() == int(grp.buf.dones[:, :E].sum())
+
+
+def test_group_env_seeds_follow_each_experiments_schedule():
+    """hwy_set_seed_groups: group g's envs reset with seed_bases[g] + l + 1 (+ E per episode),
+    so a grouped handle's first observations equal each solo handle's."""
+    from config.base_config import HIGHWAY_CONFIG
+    from hwy.vec_env import HighwayVecEnv
+
+    E, seeds = 8, [5, 900, 77]
+    grp = HighwayVecEnv(HIGHWAY_CONFIG, num_envs=E * len(seeds), device=DEV)
+    grp.set_seed_groups(seeds, E)
+    obs, _ = grp.reset()
+    obs = obs.clone()
+    for g, s in enumerate(seeds):
+        solo = HighwayVecEnv(HIGHWAY_CONFIG, num_envs=E, device=DEV)
+        solo.set_seed_schedule(s)
+        o, _ = solo.reset()
+        assert torch.equal(obs[g * E:(g + 1) * E], o), g
+        solo.close()
+    with pytest.raises(Exception):
+        grp.set_seed_groups(seeds[:2], E)  # 2 x 8 envs do not cover 24
+    grp.close()
