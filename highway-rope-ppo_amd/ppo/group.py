@@ -158,37 +158,47 @@ class ExperimentGroup:
             ag._adam_to("fused")
             fused.append(F)
         if self._upd is None or self._upd[0] != (tuple(id(F) for F in fused), mb, nmb):
+            # static inputs of the captured steps (FusedPPO's _static_bufs): advantages,
+            # returns and the mapped permutations are copied in every update
             adv_g = torch.empty(T * GE, device=self.dev)
+            ret_g = torch.empty(T * GE, device=self.dev)
             idx = torch.empty(G, n, dtype=torch.int64, device=self.dev)
             self._upd = [(tuple(id(F) for F in fused), mb, nmb), GroupStep(fused), None, adv_g,
-                         idx, None]
-        _, step, graph, adv_grp, idx_all, bound = self._upd
+                         idx, None, ret_g]
+        _, step, graph, adv_grp, idx_all, bound, ret_flat = self._upd
         adv3 = adv_grp.view(T, G, E)
+        perms = self._perms if getattr(self, "_perms", None) is not None else \
+            torch.empty(G, n, dtype=torch.int64, device=self.dev)
+        self._perms = perms
         for g, ag in enumerate(self.agents):
             # the solo update_rollout's order on this experiment's generator and samples
             a = ag.normalize_advantages(adv[:, g * E:(g + 1) * E].reshape(n))
             adv3[:, g].copy_(a.view(T, E))
-            perm = torch.randperm(n, device=self.dev, generator=ag.generator)
-            # sample (t, l) of experiment g sits at t*G*E + g*E + l of the grouped rollout
-            torch.add(torch.div(perm, E, rounding_mode="floor") * GE + g * E, perm % E,
-                      out=idx_all[g])
+            torch.randperm(n, device=self.dev, generator=ag.generator, out=perms[g])
+        # sample (t, l) of experiment g sits at t*G*E + g*E + l of the grouped rollout
+        offs = torch.arange(G, device=self.dev, dtype=torch.int64).mul_(E).view(G, 1)
+        torch.add(torch.div(perms, E, rounding_mode="floor") * GE + offs, perms % E, out=idx_all)
         states = buf.states[:T].reshape(T * GE, -1)
         pre = buf.pre_tanh.reshape(T * GE, -1)
         old_lp = buf.log_probs.reshape(T * GE)
-        ret_flat = ret.reshape(T * GE)
+        ret_flat.copy_(ret.reshape(T * GE))
         key = (states.data_ptr(), pre.data_ptr(), old_lp.data_ptr(), adv_grp.data_ptr(),
                ret_flat.data_ptr(), idx_all.data_ptr()) + tuple(F._scalar_key() for F in fused)
-        args = [[F._args(states, pre, old_lp, adv_grp, ret_flat, idx_all[g].data_ptr() + i * mb * 8)
-                 for i in range(nmb)] for g, F in enumerate(fused)]
+        if bound != key:  # the learners' argument structs and the device tables, once per key
+            self.stats["update_prepare"] += 1
+            args = [[F._args(states, pre, old_lp, adv_grp, ret_flat,
+                             idx_all[g].data_ptr() + i * mb * 8) for i in range(nmb)]
+                    for g, F in enumerate(fused)]
+            step.prepare(args)
+            graph = None
+            self._upd[2] = None
+            self._upd[5] = key
+            self._args = args
+        args = self._args
         for F, a in zip(fused, args):
             F._last_args, F._last_inputs = a, (states, pre, old_lp, adv_grp, ret_flat, idx_all)
             F.counters[1].zero_()
             F.sync_params(a[0])  # FusedPPO.run's tile-image refresh
-        if bound != key:
-            self.stats["update_prepare"] += 1
-            step.prepare(args)
-            graph = None
-            self._upd[5] = key
         epochs = self.agents[0].epochs
         if not self.use_graphs:
             for _ in range(epochs):
