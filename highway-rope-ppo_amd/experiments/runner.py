@@ -161,3 +161,66 @@ class ExperimentRunner:
                         f"Duration: {results['duration_seconds']:.2f}s")
         logging.shutdown()
         return results
+
+    def launch_group(self, exps) -> list:
+        """launch() for experiments that differ only in their seed (a sweep cell's seeds), run
+        as ONE ExperimentGroup on this runner's device (ppo/group.py: the experiments batched into
+        the env, acting and minibatch-step launches; each bit-identical to its solo launch()).
+        The reference runs such a cell as len(exps) separate processes oversubscribing the GPUs
+        (main.py:188-242, utils/device_pool.py:44-72).  Needs the vectorised loop
+        (extra["num_envs"] > 1) and the fused HIP learner; returns one status dict per experiment,
+        in order."""
+        import math
+
+        from ppo.group import build_group
+        from training.routine import train_group
+
+        exps = list(exps)
+        t0 = time.time()
+        key = {(e.condition, repr(e.hp), repr(sorted(e.extra.items())),
+                repr(e.env_config_overrides), e.max_episodes, e.target_reward) for e in exps}
+        if len(key) != 1:
+            raise ValueError("launch_group: the experiments must differ only in seed and name")
+        e0 = exps[0]
+        E = int(e0.extra.get("num_envs", 1))
+        if E <= 1:
+            raise ValueError("launch_group needs extra['num_envs'] > 1 (the vectorised loop)")
+        results = [{"experiment_name": e.name, "status": "FAILED"} for e in exps]
+        loggers = []
+        grp = None
+        try:
+            with self.pool.acquire() as device:
+                for e in exps:
+                    set_random_seeds(e.seed)  # as launch() does before the logger
+                    lg = setup_experiment_logger(e.name)
+                    lg.info(f"[{e.name}] Acquired device: {device} | Seed: {e.seed} | group of "
+                            f"{len(exps)}")
+                    loggers.append(lg)
+                T = max(1, math.ceil(e0.hp.steps_per_update / E))
+                lg_iter = iter(loggers)
+
+                def make_agent(sd):
+                    return self._create_agent(sd, 2, e0.hp, next(lg_iter), device, e0.extra)
+
+                grp = build_group(e0.condition, self.base_config, [e.seed for e in exps], E, T,
+                                  device, make_agent, d_embed=e0.hp.d_embed,
+                                  env_overrides=e0.env_config_overrides)
+                outs = train_group(grp, [e.name for e in exps], [e.seed for e in exps],
+                                   max_episodes=e0.max_episodes, target_reward=e0.target_reward,
+                                   log_interval=e0.extra.get("log_interval", 20),
+                                   eval_interval=e0.extra.get("eval_interval", 50),
+                                   loggers=loggers)
+                for res, (rewards, avg_rewards, metrics) in zip(results, outs):
+                    res.update(status="COMPLETED", rewards=rewards, avg_rewards=avg_rewards,
+                               metrics_history=metrics)
+        except Exception as ex:
+            for res in results:
+                res["error_message"] = str(ex)
+                res["error_traceback"] = traceback.format_exc()
+        finally:
+            if grp is not None:
+                grp.close()
+        for res in results:
+            res["duration_seconds"] = time.time() - t0
+        logging.shutdown()
+        return results

@@ -22,7 +22,7 @@ kernels run the solo calls' bodies per learner, so each experiment is bit for bi
 
 from __future__ import annotations
 
-from typing import List, Optional, Sequence
+from typing import Callable, List, Optional, Sequence
 
 import torch
 
@@ -236,6 +236,14 @@ class ExperimentGroup:
         self.rollout()
         return self.update(return_metrics)
 
+    def close(self) -> None:
+        """Release the grouped env handle and the experiments' own (evaluation template) envs."""
+        for e in getattr(self, "solo_envs", []) + [getattr(self, "group_env", self.env)]:
+            try:
+                e.close()
+            except Exception:
+                pass
+
     def episode_returns(self, g: int) -> torch.Tensor:
         """Returns of experiment g's episodes that ended in the last rollout, in (step, env)
         order (training/routine.py:_episode_ends on its [T, E] slice)."""
@@ -245,46 +253,44 @@ class ExperimentGroup:
         return r[d != 0]
 
 
-def build_group(condition, base_config, hp, seeds: Sequence[int], envs_per_experiment: int,
-                rollout_len: int, device: torch.device, d_embed: Optional[int] = None,
+def build_group(condition, base_config, seeds: Sequence[int], envs_per_experiment: int,
+                rollout_len: int, device: torch.device, make_agent: Callable, d_embed=None,
                 env_overrides: Optional[dict] = None, use_graphs: bool = True):
     """A group of len(seeds) experiments of one condition, each constructed as
-    experiments/runner.py constructs its solo run (set_random_seeds(seed), make_env -- whose
-    RankPE table draws from the global torch RNG --, then PPOAgent), so each experiment's
-    weights, rank table and generator are its solo run's.  hp: PPOAgent keyword arguments
-    (lr, epochs, batch_size, hidden_dim, ...)."""
+    experiments/runner.py constructs its solo run: set_random_seeds(seed), make_env (whose RankPE
+    table draws from the global torch RNG), env.to(device), then ``make_agent(state_dim)`` (the
+    PPOAgent, its weights drawn from the global RNG, its generator seeded from it), so every
+    experiment's weights, rank table and generator are its solo run's.  The experiments' own
+    E-env handles are kept as ``group.solo_envs`` (templates of their evaluation envs)."""
     import copy
 
     from experiments.wrappers import make_env
-    from hwy.vec_env import HighwayVecEnv
+    from hwy.ops import PE_RANK
     from utils.reproducibility import set_random_seeds
-    from ppo.agent import PPOAgent
 
     E = int(envs_per_experiment)
     ov = copy.deepcopy(env_overrides or {})
-    agents, tables = [], []
-    probe = None
+    agents, tables, solos = [], [], []
     for s in seeds:
         set_random_seeds(int(s))
         solo = make_env(condition, base_config, d_embed=d_embed,
-                        env_overrides=dict(ov, num_envs=E, device=device, autoreset=True))
+                        env_overrides=dict(copy.deepcopy(ov), num_envs=E, device=device,
+                                           autoreset=True))
+        if hasattr(solo, "to") and callable(solo.to):
+            solo = solo.to(device)
         base = solo.unwrapped
-        if hasattr(solo, "to"):
-            solo.to(device)
         t = getattr(base, "_pe_table", None)
         tables.append(None if t is None else t.copy())
-        sd = base.obs_rows * base.obs_features
-        agents.append(PPOAgent(sd, 2, device=device, use_graphs=use_graphs, **hp))
-        probe = solo
+        agents.append(make_agent(base.obs_rows * base.obs_features))
+        solos.append(solo)
     env = make_env(condition, base_config, d_embed=d_embed,
-                   env_overrides=dict(ov, num_envs=len(seeds) * E, device=device, autoreset=True))
-    if hasattr(env, "to"):
-        env.to(device)
-    base = env.unwrapped
-    from hwy.ops import PE_RANK
-
-    rank = base.hwy_config.pe_kind == PE_RANK and tables[0] is not None
+                   env_overrides=dict(copy.deepcopy(ov), num_envs=len(seeds) * E, device=device,
+                                      autoreset=True))
+    if hasattr(env, "to") and callable(env.to):
+        env = env.to(device)
+    rank = env.unwrapped.hwy_config.pe_kind == PE_RANK and tables[0] is not None
     grp = ExperimentGroup(agents, env, seeds, E, rollout_len, use_graphs=use_graphs,
                           rank_tables=tables if rank else None)
-    grp._keep = (probe, env)
+    grp.solo_envs = solos
+    grp.group_env = env
     return grp

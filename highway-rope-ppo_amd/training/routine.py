@@ -354,6 +354,75 @@ def _train_vector(env, agent, max_episodes, log_interval, eval_interval, steps_p
     return episode_rewards, training_episodes, total_steps
 
 
+def train_group(group, experiment_names, exp_seeds, max_episodes=500, target_reward=0.0,
+                log_interval=20, eval_interval=50, loggers=None):
+    """train_with_experiment_name for every experiment of an ExperimentGroup (ppo/group.py) at
+    once: one grouped rollout + update per iteration, then each experiment's bookkeeping exactly
+    as _train_vector does it on its own [T, E] slice (episode stream in (step, env) order,
+    evaluation every ``eval_interval`` episodes on its own eval envs, best / solved checkpoints,
+    artifacts).  An experiment that reaches ``max_episodes`` stops where its solo run stops; the
+    group keeps stepping it (its later state is never read) until every experiment is done.
+    Returns, per experiment, the reference's (rewards, avg_rewards, metrics_history), each equal
+    to its solo run's: the group's experiments are bit-identical to solo runs
+    (tests/test_group_gpu.py) and evaluation draws no random numbers."""
+    G, E, T = group.G, group.E, group.T
+    artifacts_dir = ensure_artifacts_dir()
+    checkpoint_dir = os.path.join(artifacts_dir, "checkpoints")
+    os.makedirs(checkpoint_dir, exist_ok=True)
+    start_time = time.time()
+    runs = []
+    for g in range(G):
+        name = experiment_names[g]
+        logger = loggers[g] if loggers else setup_experiment_logger(name)
+        prefix = f"[{name}]" if name else ""
+        logger.info(f"{prefix} Starting training for experiment: {name} (group of {G})")
+        mh = {"experiment_name": name, "episode_rewards": [], "eval_rewards": [],
+              "avg_eval_rewards": [], "policy_updates": [], "episode_numbers": [],
+              "eval_episode_numbers": [], "timestamps": []}
+        tracker = _EvalTracker(group.solo_envs[g], group.agents[g], int(exp_seeds[g]),
+                               target_reward, checkpoint_dir, name, mh, logger, prefix, start_time)
+        logger.info(f"{prefix} Performing initial evaluation...")
+        tracker.initial()
+        runs.append({"name": name, "logger": logger, "prefix": prefix, "mh": mh,
+                     "tracker": tracker, "episode_rewards": [], "training_episodes": [],
+                     "episode_num": 0, "total_steps": 0, "done": max_episodes <= 0})
+    buf = group.buf
+    while not all(r["done"] for r in runs):
+        t_update = time.time()
+        group.rollout()
+        upds = group.update(return_metrics=True)
+        for g, r in enumerate(runs):
+            if r["done"]:
+                continue
+            r["total_steps"] += T * E
+            sl = slice(g * E, (g + 1) * E)
+            for ret in _episode_ends(buf.dones[:, sl], buf.ep_return[:, sl]):
+                if r["episode_num"] >= max_episodes:
+                    break
+                r["episode_num"] += 1
+                ret = float(ret)
+                r["episode_rewards"].append(ret)
+                r["training_episodes"].append(r["episode_num"])
+                r["mh"]["episode_rewards"].append(ret)
+                r["mh"]["episode_numbers"].append(r["episode_num"])
+                _log_episode(r["logger"], r["prefix"], r["episode_num"], ret, r["episode_rewards"],
+                             log_interval, r["total_steps"], start_time)
+                if r["episode_num"] % eval_interval == 0:
+                    r["tracker"].on_episode(r["episode_num"])
+            r["mh"]["policy_updates"].append({"episode": r["episode_num"], "steps": T * E,
+                                              "time": time.time() - t_update, **upds[g]})
+            if r["episode_num"] >= max_episodes:
+                r["done"] = True
+    out = []
+    for r in runs:
+        tr = r["tracker"]
+        _save_artifacts(artifacts_dir, checkpoint_dir, r["name"], r["mh"], r["training_episodes"],
+                        r["episode_rewards"], tr.eval_episodes, tr.rewards, tr.avg_rewards,
+                        target_reward, r["total_steps"], r["logger"], r["prefix"])
+        out.append((tr.rewards, tr.avg_rewards, r["mh"]))
+    return out
+
+
 def _rank_world(group):
     if group is None:
         return 0, 1

@@ -58,7 +58,10 @@ def test_group_matches_solo_runs_bit_for_bit(cond_name, d, H, order):
     cond = Condition[cond_name]
     seeds, E, T, iters = [42, 1042, 2042], 16, 16, 3
     overrides = {} if order is None else {"observation": {"order": order}}
-    grp = build_group(cond, HIGHWAY_CONFIG, _hp(H), seeds, E, T, DEV, d_embed=d,
+    from ppo.agent import PPOAgent
+
+    grp = build_group(cond, HIGHWAY_CONFIG, seeds, E, T, DEV,
+                      lambda sd: PPOAgent(sd, 2, device=DEV, **_hp(H)), d_embed=d,
                       env_overrides=overrides)
     ghist, gmet = [], []
     for _ in range(iters):
@@ -107,3 +110,37 @@ def test_group_env_seeds_follow_each_experiments_schedule():
     with pytest.raises(Exception):
         grp.set_seed_groups(seeds[:2], E)  # 2 x 8 envs do not cover 24
     grp.close()
+
+
+def test_runner_launch_group_equals_launch(tmp_path, monkeypatch):
+    """ExperimentRunner.launch_group (one ExperimentGroup for a cell's seeds) returns, per
+    experiment, exactly what launch() returns for it alone: the episode stream, every
+    evaluation and the moving averages (training/routine.py:train_group vs _train_vector)."""
+    from config.base_config import HIGHWAY_CONFIG
+    from experiments.config import Condition, ConditionHP, Experiment
+    from experiments.runner import ExperimentRunner
+
+    monkeypatch.chdir(tmp_path)
+
+    def exp(seed):
+        hp = ConditionHP(lr=3e-4, clip_eps=0.2, epochs=2, batch_size=64, hidden_dim=256,
+                         d_embed=4)
+        hp.entropy_coef = 0.005
+        hp.steps_per_update = 16 * 32
+        return Experiment(name=f"grp_rank_seed{seed}", condition=Condition.SHUFFLED_RANKPE,
+                          hp=hp, seed=seed, max_episodes=24, target_reward=1e9,
+                          extra={"num_envs": 16, "num_minibatches": 8, "eval_interval": 8,
+                                 "log_interval": 50}, env_config_overrides={})
+
+    seeds = [42, 1042]
+    grouped = ExperimentRunner(HIGHWAY_CONFIG).launch_group([exp(s) for s in seeds])
+    for s, g in zip(seeds, grouped):
+        solo = ExperimentRunner(HIGHWAY_CONFIG).launch(exp(s))
+        assert solo["status"] == g["status"] == "COMPLETED", (solo.get("error_message"),
+                                                              g.get("error_message"))
+        assert g["rewards"] == solo["rewards"] and g["avg_rewards"] == solo["avg_rewards"], s
+        mg, ms = g["metrics_history"], solo["metrics_history"]
+        assert mg["episode_rewards"] == ms["episode_rewards"]
+        assert mg["eval_episode_numbers"] == ms["eval_episode_numbers"]
+        assert [u["loss"] for u in mg["policy_updates"]] == [u["loss"] for u in ms["policy_updates"]]
+    assert (tmp_path / "artifacts").exists() or any(tmp_path.iterdir())

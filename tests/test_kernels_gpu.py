@@ -1,4 +1,7 @@
-"""Device math library, stand-alone PE kernel and GAE kernel vs the CPU oracle (bit-exact)."""
+"""Device math library, stand-alone PE kernel and GAE kernel vs the CPU oracle (bit-exact), and
+the device math library against libm / numpy in float64."""
+
+import math
 
 import numpy as np
 import pytest
@@ -69,6 +72,38 @@ def test_math_library_bit_exact(op):
     # NaN payloads differ between the host and the device (x86 vs gfx950 default NaN): NaN == NaN
     bad = np.nonzero((host.view(np.uint32) != dev.view(np.uint32)) & ~(np.isnan(host) & np.isnan(dev)))[0]
     assert bad.size == 0, f"op {op}: {bad.size} mismatches, e.g. x={x[bad[0]]!r} host={host[bad[0]]!r} dev={dev[bad[0]]!r}"
+
+
+@pytest.mark.parametrize("op,fn,lo,hi,tol", [
+    (0, math.sin, -20, 20, 2e-7), (1, math.cos, -20, 20, 2e-7), (3, math.atan, -50, 50, 2e-7),
+    (4, math.asin, -1, 1, 3e-7), (5, math.exp, -30, 30, 3e-7), (6, math.log, 1e-3, 1e4, 3e-7),
+    (2, math.tan, -1.2, 1.2, 6e-7),
+])
+def test_device_math_accuracy_against_libm(op, fn, lo, hi, tol):
+    """The DEVICE math library against libm in float64: the env kernel and
+    the oracle share hwy_math.h, so their bit-exact agreement cannot catch a math-library bug;
+    this pins what the gfx950 build computes against an independent reference, at the CPU
+    accuracy test's bounds (tests/test_oracle_golden.py), on the ranges the step uses."""
+    x = np.random.default_rng(100 + op).uniform(lo, hi, 200000).astype(np.float32)
+    got = ops.math_selftest(op, torch.as_tensor(x, device=DEV)).cpu().numpy().astype(np.float64)
+    want = np.array([fn(float(v)) for v in x])
+    err = np.abs(got - want) / np.maximum(np.abs(want), 1e-30)
+    absok = np.abs(got - want) <= 1e-7
+    assert np.all((err <= tol) | absok), (float(err.max()), x[np.argmax(err)])
+
+
+def test_device_pow_and_idm_pow_against_numpy():
+    """hm_powf (op 7) and the IDM's hm_powf_idm (op 15) on the device against float64 np.power
+    over the IDM's bases (max(v, 0) / v0 <= 2.5) and exponents (DELTA in [3.5, 4.5])."""
+    rng = np.random.default_rng(77)
+    b = rng.uniform(0, 2.5, 100000).astype(np.float32)
+    p = rng.uniform(3.5, 4.5, 100000).astype(np.float32)
+    want = np.power(b.astype(np.float64), p.astype(np.float64))
+    for op in (7, 15):
+        got = ops.math_selftest(op, torch.as_tensor(b, device=DEV),
+                                torch.as_tensor(p, device=DEV)).cpu().numpy().astype(np.float64)
+        rel = np.abs(got - want) / np.maximum(want, 1e-30)
+        assert (rel[want > 1e-30] < 1e-5).all(), (op, float(rel.max()))
 
 
 @pytest.mark.parametrize("kind,d", [(_abi.PE_NONE, 0), (_abi.PE_ROPE, 4), (_abi.PE_ROPE, 2),
