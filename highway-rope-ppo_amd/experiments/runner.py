@@ -110,6 +110,7 @@ class ExperimentRunner:
                 logger.info(f"[{exp.name}] Acquired device: {device} | Seed: {exp.seed}")
                 logger.info(f"[{exp.name}] Condition: {exp.condition.name} | HPs: {exp.hp}")
                 env = None
+                agent = None
                 try:
                     overrides = dict(exp.env_config_overrides)
                     if "num_envs" in exp.extra:
@@ -150,6 +151,9 @@ class ExperimentRunner:
                     results["error_message"] = str(e)
                     results["error_traceback"] = traceback.format_exc()
                 finally:
+                    # graphs holding RCCL collectives are freed while the communicator lives
+                    if agent is not None and getattr(agent, "_fused", None) is not None:
+                        agent._fused.release_graphs()
                     if env is not None:
                         env.close()
         except Exception as e:

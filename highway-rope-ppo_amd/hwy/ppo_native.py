@@ -493,6 +493,20 @@ class FusedPPO:
         self._tiles_version = self._param_versions()
         return dict(zip(self.KERNELS + ("launch_floor",), (float(u) for u in us)))
 
+    def release_graphs(self) -> None:
+        """Drop the captured epoch / step graphs now (after the stream has drained).  Call it
+        before tearing down the process group an RCCL-captured graph was built on: a graph whose
+        collective outlives its communicator aborts in its destructor ("operation not permitted
+        when stream is capturing"), and a graph in a reference cycle (agent <-> FusedPPO) is
+        otherwise freed at an arbitrary later point."""
+        torch.cuda.synchronize()
+        self._graphs = None
+        self._bound_key = None
+        self._captured_collectives = False
+        import gc
+
+        gc.collect()
+
     def _epoch_event(self, start=None):
         if self.epoch_events is None:
             return None

@@ -22,6 +22,9 @@
  *                                DistanceEmbedWrapper.observation        experiments/dist_embed.py:76-96
  *                                RankEmbedWrapper.observation            experiments/rank_embed.py:45-51
  *   hwy_gae                   <- PPOMemory.compute_advantages            ppo/agent.py:126-138
+ *   hwy_set_seed_groups       <- one gym.make per experiment of a sweep  experiments/runner.py:73-78
+ *                                (main.py:188-242 fans the seeds out as separate processes; here
+ *                                 a cell's seeds share one handle, each with its own schedule)
  *
  * Conventions
  *   - Plain pointers and sizes only; device pointers are HIP device pointers (e.g. torch

@@ -119,6 +119,9 @@ def _rccl1_worker(rank, port, out_dir):
         torch.cuda.synchronize()
         out[tag] = {"state": {k: v.cpu() for k, v in agent.actor_critic.state_dict().items()},
                     "captured": F._captured_collectives}
+        # graphs holding RCCL collectives are freed while the communicator lives (the agent <->
+        # FusedPPO cycle would otherwise free them after destroy_process_group: abort)
+        F.release_graphs()
     torch.save(out, os.path.join(out_dir, "rccl1.pt"))
     torch.distributed.destroy_process_group()
 

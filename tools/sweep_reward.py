@@ -8,11 +8,13 @@ launches, each bit-identical to its solo launch()), at the recipe of tools/train
 --num-envs 16 --rollout 128 --minibatches 32 --episodes 1500 --eval-interval 50 (the reference's
 2,048 samples per update in minibatches of 64, 8 epochs, lr 3e-4).
 
-Each run's final_reward is compared with the solo runs of the same recipe and seed recorded in
+Each cell writes OUT/<condition>_h<H>_e<E>_t<T>/summary.jsonl (the layout tools/recipe_stats.py
+and tools/condition_order.py read; run them afterwards -- no child process is started from this
+GPU process).  Each run's final_reward is compared with the solo runs of the same recipe and seed recorded in
 round 4 (profiles/r4/reward/<cell>_e16_t128/summary.jsonl, one ExperimentRunner.launch per
 process-sequential run): every kernel change since is bit-identical, so the grouped sweep must
-reproduce them exactly.  Writes OUT/<cell>/summary.jsonl (train_parity.py's row format),
-OUT/sweep.json (wall time, per-cell agreement) and prints one line per cell.
+reproduce them exactly.  Also writes OUT/sweep.json (wall time, per-cell agreement) and prints
+one line per cell.
 
     python tools/sweep_reward.py --out gpurun_out/sweep_reward [--cells sorted_h256 ...]
 """
@@ -80,7 +82,7 @@ def main():
             exps.append(Experiment(name=name, condition=conds[cname], hp=hp, seed=seed,
                                    max_episodes=args.episodes, target_reward=130.0, extra=extra,
                                    env_config_overrides={}))
-        run_dir = os.path.join(out, cell)
+        run_dir = os.path.join(out, f"{cname}_h{H}_e{E}_t{T}")  # tools/condition_order.py layout
         os.makedirs(run_dir, exist_ok=True)
         cwd = os.getcwd()
         os.chdir(run_dir)
