@@ -2537,20 +2537,33 @@ __global__ void __launch_bounds__(256) ppo_adam_tiles(OptArgs o) { adam_tiles_bo
 // sweep's seeds of one condition).  Workgroup (x, y) runs the solo kernel's workgroup x for
 // learner y, whose arguments the kernel reads from a device table (hwy_ppo_group_prepare): the
 // same bodies and tile shapes as the solo launches, so each learner's bits are its solo run's.
+// a learner's own grid of each grouped launch (the launch covers the largest learner's)
+struct GroupLim {
+  int rows, wgrad, wsum, adam;
+};
+
 template <int QH, int NW, int RT>
-__global__ void __launch_bounds__(64 * NW, 1) ppo_rows_grp(const RowArgs* __restrict__ tab) {
+__global__ void __launch_bounds__(64 * NW, 1) ppo_rows_grp(const RowArgs* __restrict__ tab,
+                                                           const GroupLim* __restrict__ lim) {
+  if ((int)blockIdx.x >= lim[blockIdx.y].rows) return;  // whole workgroup
   rows_body<QH, NW, RT, false>(tab[blockIdx.y]);
 }
 
-__global__ void __launch_bounds__(512) ppo_wgrad_grp(const WgArgs* __restrict__ tab) {
+__global__ void __launch_bounds__(512) ppo_wgrad_grp(const WgArgs* __restrict__ tab,
+                                                     const GroupLim* __restrict__ lim) {
+  if ((int)blockIdx.x >= lim[blockIdx.y].wgrad) return;
   ppo_wgrad_body(tab[blockIdx.y]);
 }
 
-__global__ void __launch_bounds__(256) ppo_wsum_grp(const WgArgs* __restrict__ tab) {
+__global__ void __launch_bounds__(256) ppo_wsum_grp(const WgArgs* __restrict__ tab,
+                                                    const GroupLim* __restrict__ lim) {
+  if ((int)blockIdx.x >= lim[blockIdx.y].wsum) return;
   wsum_body(tab[blockIdx.y]);
 }
 
-__global__ void __launch_bounds__(256) ppo_adam_tiles_grp(const OptArgs* __restrict__ tab) {
+__global__ void __launch_bounds__(256) ppo_adam_tiles_grp(const OptArgs* __restrict__ tab,
+                                                          const GroupLim* __restrict__ lim) {
+  if ((int)blockIdx.x >= lim[blockIdx.y].adam) return;
   adam_tiles_body(tab[blockIdx.y]);
 }
 
@@ -3015,40 +3028,63 @@ int hwy_ppo_act(const hwy_ppo_act_args* a, void* stream) {
 }
 
 // ---- grouped learners (include/hwy_ppo.h): the device table of one minibatch step is
-// [G RowArgs | G WgArgs | G OptArgs], each section 256-byte aligned
+// [G RowArgs | G WgArgs | G OptArgs | G GroupLim], each section 256-byte aligned.  The learners
+// share B and H (so every learner takes the 16-row tiles and the same row-kernel grid); their
+// state dims may differ, which changes the weight-gradient tile count and Adam's W1 blocks, so
+// each launch covers the largest learner's grid and a learner's surplus workgroups exit.
 static int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
 static int64_t grp_row_off(int) { return 0; }
 static int64_t grp_wg_off(int G) { return align256((int64_t)G * sizeof(RowArgs)); }
 static int64_t grp_opt_off(int G) { return grp_wg_off(G) + align256((int64_t)G * sizeof(WgArgs)); }
+static int64_t grp_lim_off(int G) { return grp_opt_off(G) + align256((int64_t)G * sizeof(OptArgs)); }
 
 static bool group_dims_ok(const hwy_ppo_dims& d) {
   if (hwy_ppo_workspace_bytes(&d) < 0 || !fused_ok(d) || d.A != 2 || d.B < 1) return false;
   char* base = reinterpret_cast<char*>(uintptr_t(1) << 20);  // carve only adds offsets to it
   const Work w = carve(d, base, nullptr);
-  return w.fused && w.rt == kRowTile;  // 16-row tiles: minibatches below the 32-row threshold
+  // 16-row tiles (minibatches below the 32-row threshold) and one workgroup per (tile, slice):
+  // the balanced weight-gradient partition reads gridDim.x, which the grouped launch widens
+  return w.fused && w.rt == kRowTile && !w.bal;
+}
+
+// one learner's grids (the solo launches'): rows, ppo_wgrad, ppo_wsum, ppo_adam_tiles
+static GroupLim group_lim(const hwy_ppo_dims& d) {
+  char* base = reinterpret_cast<char*>(uintptr_t(1) << 20);
+  const Work w = carve(d, base, nullptr);
+  hwy_ppo_args geom = {};
+  geom.dims = d;
+  const OptArgs og = opt_args(geom, make_layout(d), w);
+  GroupLim l;
+  l.rows = w.n1, l.wgrad = w.grid2, l.wsum = (w.tac + w.t2 + w.t1) * (kWgTM * kWgTN / 1024);
+  l.adam = adam_tiles_grid(og);
+  return l;
 }
 
 int64_t hwy_ppo_group_table_bytes(const hwy_ppo_dims* d, int G) {
   if (!d || G < 1 || !group_dims_ok(*d)) return -1;
-  return grp_opt_off(G) + align256((int64_t)G * sizeof(OptArgs));
+  return grp_lim_off(G) + align256((int64_t)G * sizeof(GroupLim));
 }
 
-int hwy_ppo_group_prepare(const hwy_ppo_args* a, int G, void* table, void* stream) {
-  if (!a || G < 1 || !table) return -1;
-  const hwy_ppo_dims& d = a[0].dims;
-  if (!group_dims_ok(d)) return -1;
-  const Layout L = make_layout(d);
-  const int64_t bytes = hwy_ppo_group_table_bytes(&d, G);
+int hwy_ppo_group_prepare(const hwy_ppo_args* a, int G, void* table, hwy_ppo_group_plan* plan,
+                          void* stream) {
+  if (!a || G < 1 || !table || !plan) return -1;
+  const hwy_ppo_dims& d0 = a[0].dims;
+  if (!group_dims_ok(d0)) return -1;
+  const int64_t bytes = hwy_ppo_group_table_bytes(&d0, G);
   char* host = static_cast<char*>(calloc((size_t)bytes, 1));
   if (!host) return -2;
+  hwy_ppo_group_plan p = {};
+  p.G = G, p.B = d0.B, p.H = d0.H;
   int rc = 0;
   for (int g = 0; g < G && rc == 0; ++g) {
     const hwy_ppo_args& ag = a[g];
-    if (memcmp(&ag.dims, &d, sizeof(d)) != 0 || ag.grads_modified || !ag.workspace ||
-        !ag.counters || !ag.params || !ag.grads || !ag.adam_m || !ag.adam_v) {
+    const hwy_ppo_dims& d = ag.dims;
+    if (d.B != d0.B || d.H != d0.H || d.A != d0.A || !group_dims_ok(d) || ag.grads_modified ||
+        !ag.workspace || !ag.counters || !ag.params || !ag.grads || !ag.adam_m || !ag.adam_v) {
       rc = -1;
       break;
     }
+    const Layout L = make_layout(d);
     const Work w = carve(d, ag.workspace, nullptr);
     const OptArgs o = opt_args(ag, L, w);
     if (!adam_tiles_ok(ag, o, w)) {
@@ -3058,46 +3094,48 @@ int hwy_ppo_group_prepare(const hwy_ppo_args* a, int G, void* table, void* strea
     reinterpret_cast<RowArgs*>(host + grp_row_off(G))[g] = row_args(ag, L, w);
     reinterpret_cast<WgArgs*>(host + grp_wg_off(G))[g] = wg_args(ag, L, w);
     reinterpret_cast<OptArgs*>(host + grp_opt_off(G))[g] = o;
+    const GroupLim l = group_lim(d);
+    reinterpret_cast<GroupLim*>(host + grp_lim_off(G))[g] = l;
+    p.grid_rows = std::max(p.grid_rows, l.rows), p.grid_wgrad = std::max(p.grid_wgrad, l.wgrad);
+    p.grid_wsum = std::max(p.grid_wsum, l.wsum), p.grid_adam = std::max(p.grid_adam, l.adam);
   }
   hipStream_t s = (hipStream_t)stream;
   if (rc == 0 && (hipMemcpyAsync(table, host, (size_t)bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
                   hipStreamSynchronize(s) != hipSuccess))
     rc = -2;
   free(host);
+  if (rc == 0) *plan = p;
   return rc;
 }
 
-int hwy_ppo_group_step(const hwy_ppo_dims* d, int G, const void* table, void* stream) {
-  if (!d || G < 1 || !table || !group_dims_ok(*d)) return -1;
-  char* base = reinterpret_cast<char*>(uintptr_t(1) << 20);
-  const Work w = carve(*d, base, nullptr);
-  const Layout L = make_layout(*d);
-  hwy_ppo_args geom = {};
-  geom.dims = *d;
-  const OptArgs og = opt_args(geom, L, w);  // the grid geometry only
+int hwy_ppo_group_step(const hwy_ppo_group_plan* plan, const void* table, void* stream) {
+  if (!plan || !table || plan->G < 1 || plan->H < 64 || plan->H > 512 || plan->H % 64 ||
+      plan->grid_rows < 1 || plan->grid_wgrad < 1 || plan->grid_wsum < 1 || plan->grid_adam < 1)
+    return -1;
+  const int G = plan->G;
   const char* t = static_cast<const char*>(table);
   const RowArgs* tr = reinterpret_cast<const RowArgs*>(t + grp_row_off(G));
   const WgArgs* tw = reinterpret_cast<const WgArgs*>(t + grp_wg_off(G));
   const OptArgs* to = reinterpret_cast<const OptArgs*>(t + grp_opt_off(G));
+  const GroupLim* tl = reinterpret_cast<const GroupLim*>(t + grp_lim_off(G));
   hipStream_t s = (hipStream_t)stream;
-  const dim3 g1(w.n1, G), b4(256), b8(512);
-  switch (d->H / 64) {
-    case 1: hipLaunchKernelGGL((ppo_rows_grp<1, 4, 16>), g1, b4, 0, s, tr); break;
-    case 2: hipLaunchKernelGGL((ppo_rows_grp<2, 8, 16>), g1, b8, 0, s, tr); break;
-    case 3: hipLaunchKernelGGL((ppo_rows_grp<3, 4, 16>), g1, b4, 0, s, tr); break;
-    case 4: hipLaunchKernelGGL((ppo_rows_grp<4, 8, 16>), g1, b8, 0, s, tr); break;
-    case 5: hipLaunchKernelGGL((ppo_rows_grp<5, 4, 16>), g1, b4, 0, s, tr); break;
-    case 6: hipLaunchKernelGGL((ppo_rows_grp<6, 8, 16>), g1, b8, 0, s, tr); break;
-    case 7: hipLaunchKernelGGL((ppo_rows_grp<7, 4, 16>), g1, b4, 0, s, tr); break;
-    default: hipLaunchKernelGGL((ppo_rows_grp<8, 8, 16>), g1, b8, 0, s, tr); break;
+  const dim3 g1(plan->grid_rows, G), b4(256), b8(512);
+  switch (plan->H / 64) {
+    case 1: hipLaunchKernelGGL((ppo_rows_grp<1, 4, 16>), g1, b4, 0, s, tr, tl); break;
+    case 2: hipLaunchKernelGGL((ppo_rows_grp<2, 8, 16>), g1, b8, 0, s, tr, tl); break;
+    case 3: hipLaunchKernelGGL((ppo_rows_grp<3, 4, 16>), g1, b4, 0, s, tr, tl); break;
+    case 4: hipLaunchKernelGGL((ppo_rows_grp<4, 8, 16>), g1, b8, 0, s, tr, tl); break;
+    case 5: hipLaunchKernelGGL((ppo_rows_grp<5, 4, 16>), g1, b4, 0, s, tr, tl); break;
+    case 6: hipLaunchKernelGGL((ppo_rows_grp<6, 8, 16>), g1, b8, 0, s, tr, tl); break;
+    case 7: hipLaunchKernelGGL((ppo_rows_grp<7, 4, 16>), g1, b4, 0, s, tr, tl); break;
+    default: hipLaunchKernelGGL((ppo_rows_grp<8, 8, 16>), g1, b8, 0, s, tr, tl); break;
   }
   int rc = hipGetLastError() == hipSuccess ? 0 : -1;
-  hipLaunchKernelGGL(ppo_wgrad_grp, dim3(w.grid2, G), dim3(64 * kWgWaves), 0, s, tw);
+  hipLaunchKernelGGL(ppo_wgrad_grp, dim3(plan->grid_wgrad, G), dim3(64 * kWgWaves), 0, s, tw, tl);
   rc |= hipGetLastError() == hipSuccess ? 0 : -1;
-  hipLaunchKernelGGL(ppo_wsum_grp, dim3((w.tac + w.t2 + w.t1) * (kWgTM * kWgTN / 1024), G),
-                     dim3(256), 0, s, tw);
+  hipLaunchKernelGGL(ppo_wsum_grp, dim3(plan->grid_wsum, G), dim3(256), 0, s, tw, tl);
   rc |= hipGetLastError() == hipSuccess ? 0 : -1;
-  hipLaunchKernelGGL(ppo_adam_tiles_grp, dim3(adam_tiles_grid(og), G), dim3(256), 0, s, to);
+  hipLaunchKernelGGL(ppo_adam_tiles_grp, dim3(plan->grid_adam, G), dim3(256), 0, s, to, tl);
   rc |= hipGetLastError() == hipSuccess ? 0 : -1;
   return rc;
 }
@@ -3110,22 +3148,23 @@ int hwy_ppo_group_act_prepare(const hwy_ppo_act_args* a, int G, void* table, voi
   if (!a || G < 1 || !table) return -1;
   const hwy_ppo_dims& d = a[0].dims;
   if (!fused_ok(d) || d.A != 2 || d.B < 1) return -1;
-  const Layout L = make_layout(d);
   const int64_t bytes = hwy_ppo_group_act_table_bytes(G);
   char* host = static_cast<char*>(calloc((size_t)bytes, 1));
   if (!host) return -2;
   int rc = 0;
   for (int g = 0; g < G; ++g) {
     const hwy_ppo_act_args& ag = a[g];
-    if (memcmp(&ag.dims, &d, sizeof(d)) != 0 || !ag.states || !ag.params || !ag.action ||
-        !ag.pre_tanh || !ag.logp || !ag.value || (!ag.tiles) != (!a[0].tiles) ||
-        (!ag.noise) != (!a[0].noise)) {
+    // the learners share B and H (the kernel and its grid); S may differ per learner
+    if (ag.dims.B != d.B || ag.dims.H != d.H || ag.dims.A != d.A || !fused_ok(ag.dims) ||
+        !ag.states || !ag.params || !ag.action || !ag.pre_tanh || !ag.logp || !ag.value ||
+        (!ag.tiles) != (!a[0].tiles) || (!ag.noise) != (!a[0].noise)) {
       rc = -1;
       break;
     }
+    const Layout Lg = make_layout(ag.dims);
     ActArgs r = {};
-    r.B = d.B, r.S = d.S, r.states = ag.states, r.params = ag.params, r.noise = ag.noise;
-    for (int i = 0; i < 13; ++i) r.off[i] = L.off[i];
+    r.B = d.B, r.S = ag.dims.S, r.states = ag.states, r.params = ag.params, r.noise = ag.noise;
+    for (int i = 0; i < 13; ++i) r.off[i] = Lg.off[i];
     r.action = ag.action, r.pre_tanh = ag.pre_tanh, r.logp = ag.logp, r.value = ag.value;
     r.tiles = ag.tiles;
     reinterpret_cast<ActArgs*>(host)[g] = r;

@@ -13,10 +13,13 @@ forward used for acting see the same storage) and runs one update's minibatch st
 from __future__ import annotations
 
 import ctypes
+import gc
 import os
 from typing import List, Optional
 
 import torch
+
+from utils.graphs import capture as graph_capture
 
 from .native import check, lib, stream_ptr
 
@@ -78,12 +81,6 @@ def _bind(L):
     # grouped learners (include/hwy_ppo.h)
     L.hwy_ppo_group_table_bytes.argtypes = [ctypes.POINTER(PpoDims), ctypes.c_int]
     L.hwy_ppo_group_table_bytes.restype = ctypes.c_int64
-    L.hwy_ppo_group_prepare.argtypes = [ctypes.POINTER(PpoArgs), ctypes.c_int, ctypes.c_void_p,
-                                        ctypes.c_void_p]
-    L.hwy_ppo_group_prepare.restype = ctypes.c_int
-    L.hwy_ppo_group_step.argtypes = [ctypes.POINTER(PpoDims), ctypes.c_int, ctypes.c_void_p,
-                                     ctypes.c_void_p]
-    L.hwy_ppo_group_step.restype = ctypes.c_int
     L.hwy_ppo_group_act_table_bytes.argtypes = [ctypes.c_int]
     L.hwy_ppo_group_act_table_bytes.restype = ctypes.c_int64
     L.hwy_ppo_group_act_prepare.argtypes = [ctypes.POINTER(PpoActArgs), ctypes.c_int,
@@ -503,8 +500,6 @@ class FusedPPO:
         self._graphs = None
         self._bound_key = None
         self._captured_collectives = False
-        import gc
-
         gc.collect()
 
     def _epoch_event(self, start=None):
@@ -526,17 +521,18 @@ class FusedPPO:
         with torch.cuda.stream(s):
             if self.group is None:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=s):
+                with graph_capture(g, stream=s):
                     for a in args:
                         self._fwd_bwd(a)
                         self._opt(a)
                 graphs.append(g)
             else:
+                gc.collect()
                 for a in args:
                     gf, go = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(gf, stream=s):
+                    with graph_capture(gf, stream=s, collect=False):
                         self._fwd_bwd(a)
-                    with torch.cuda.graph(go, stream=s):
+                    with graph_capture(go, stream=s, collect=False):
                         self._opt(a)
                     graphs.append((gf, go))
         torch.cuda.current_stream().wait_stream(s)
@@ -556,7 +552,7 @@ class FusedPPO:
         try:
             with torch.cuda.stream(s):
                 # thread_local: the process group's watchdog thread may query events meanwhile
-                with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+                with graph_capture(g, stream=s, capture_error_mode="thread_local"):
                     for a in args:
                         self._fwd_bwd(a)
                         self._allreduce()
@@ -572,20 +568,41 @@ class FusedPPO:
 
 
 # ------------------------------------------------------------------ grouped learners
+class PpoGroupPlan(ctypes.Structure):
+    _fields_ = [("G", ctypes.c_int32), ("B", ctypes.c_int32), ("H", ctypes.c_int32),
+                ("grid_rows", ctypes.c_int32), ("grid_wgrad", ctypes.c_int32),
+                ("grid_wsum", ctypes.c_int32), ("grid_adam", ctypes.c_int32)]
+
+
+def _bind_group(L):
+    if getattr(L, "_grp_bound", False):
+        return L
+    L.hwy_ppo_group_prepare.argtypes = [ctypes.POINTER(PpoArgs), ctypes.c_int, ctypes.c_void_p,
+                                        ctypes.POINTER(PpoGroupPlan), ctypes.c_void_p]
+    L.hwy_ppo_group_prepare.restype = ctypes.c_int
+    L.hwy_ppo_group_step.argtypes = [ctypes.POINTER(PpoGroupPlan), ctypes.c_void_p,
+                                     ctypes.c_void_p]
+    L.hwy_ppo_group_step.restype = ctypes.c_int
+    L._grp_bound = True
+    return L
+
+
 class GroupAct:
-    """ActorCritic.act for G agents of the same dims in ONE launch (hwy_ppo_group_act): agent g
-    acts on rows [g*B, (g+1)*B) of `states` and writes the same rows of the outputs, each
-    bit for bit what fused_act(agent g, its rows) writes.  The kernel arguments live in a device
-    table prepared once per (buffers, weights) key, so the launch is graph-capturable."""
+    """ActorCritic.act for G agents (same hidden width and rows per agent; state dims may
+    differ) in ONE launch (hwy_ppo_group_act): agent g acts on its own B rows and writes its own
+    output rows, each bit for bit what fused_act(agent g, its rows) writes.  The kernel arguments
+    live in a device table prepared once per (buffers, weights) key, so the launch is
+    graph-capturable."""
 
     def __init__(self, agents, B: int):
         self.agents = list(agents)
         self.G, self.B = len(self.agents), int(B)
         self.L = _bind(lib())
-        ac = self.agents[0].actor_critic
-        self.S = ac.shared[0].weight.shape[1]
-        self.H = ac.shared[0].weight.shape[0]
-        self.dims = PpoDims(self.B, self.S, self.H, 2)
+        self.S = [ag.actor_critic.shared[0].weight.shape[1] for ag in self.agents]
+        self.H = self.agents[0].actor_critic.shared[0].weight.shape[0]
+        if any(ag.actor_critic.shared[0].weight.shape[0] != self.H for ag in self.agents):
+            raise ValueError("grouped acting needs one hidden width")
+        self.dims = PpoDims(self.B, self.S[0], self.H, 2)
         nb = self.L.hwy_ppo_group_act_table_bytes(self.G)
         self.dev = self.agents[0].device
         self._tables = {}
@@ -593,32 +610,24 @@ class GroupAct:
 
     def tiles(self):
         out = []
-        for ag in self.agents:
+        for ag, S in zip(self.agents, self.S):
             flat = flat_params(ag)[0]
-            out.append(act_tiles(ag, flat, self.S, self.H))
+            out.append(act_tiles(ag, flat, S, self.H))
         return out
 
-    def table(self, states, noise, out, tiles) -> torch.Tensor:
-        """The device argument table for these buffers (cached by their addresses)."""
-        action, pre, logp, value = out
-        key = (states.data_ptr(), None if noise is None else noise.data_ptr(),
-               action.data_ptr(), pre.data_ptr(), logp.data_ptr(), value.data_ptr(), tuple(tiles),
-               tuple(flat_params(ag)[0].data_ptr() for ag in self.agents))
+    def table(self, rows, tiles) -> torch.Tensor:
+        """The device argument table for these row addresses (cached by them): rows[g] =
+        (states, noise or None, action, pre_tanh, logp, value) device addresses of agent g."""
+        key = (tuple(rows), tuple(tiles), tuple(flat_params(ag)[0].data_ptr() for ag in self.agents))
         t = self._tables.get(key)
         if t is not None:
             return t
-        B = self.B
         arr = (PpoActArgs * self.G)()
-        for g, (ag, tl) in enumerate(zip(self.agents, tiles)):
+        for g, (ag, tl, r, S) in enumerate(zip(self.agents, tiles, rows, self.S)):
             a = arr[g]
-            a.dims = self.dims
-            a.states = states.data_ptr() + g * B * self.S * 4
+            a.dims = PpoDims(self.B, S, self.H, 2)
+            a.states, a.noise, a.action, a.pre_tanh, a.logp, a.value = r
             a.params = flat_params(ag)[0].data_ptr()
-            a.noise = None if noise is None else noise.data_ptr() + g * B * 2 * 4
-            a.action = action.data_ptr() + g * B * 2 * 4
-            a.pre_tanh = pre.data_ptr() + g * B * 2 * 4
-            a.logp = logp.data_ptr() + g * B * 4
-            a.value = value.data_ptr() + g * B * 4
             a.tiles = tl
         t = torch.empty(self._nb, dtype=torch.uint8, device=self.dev)
         check(self.L.hwy_ppo_group_act_prepare(arr, self.G, t.data_ptr(), stream_ptr()),
@@ -626,48 +635,70 @@ class GroupAct:
         self._tables[key] = t
         return t
 
-    def __call__(self, states, out, noise=None, tiles=None):
-        """states [G*B, S]; out = (action [G*B,2], pre_tanh [G*B,2], logp [G*B], value [G*B]);
-        noise [G*B, 2] or None (deterministic)."""
+    def rows_of(self, states, out, noise=None, first: int = 0, count: Optional[int] = None):
+        """Row addresses of agents first..first+count acting on consecutive B-row blocks of one
+        buffer set: states [count*B, S], out = (action [.,2], pre_tanh [.,2], logp [.], value [.]),
+        noise [count*B, 2] or None."""
+        count = self.G - first if count is None else count
+        action, pre, logp, value = out
+        B, S = self.B, self.S[first]
+        rows = []
+        for g in range(count):
+            rows.append((states.data_ptr() + g * B * S * 4,
+                         None if noise is None else noise.data_ptr() + g * B * 2 * 4,
+                         action.data_ptr() + g * B * 2 * 4, pre.data_ptr() + g * B * 2 * 4,
+                         logp.data_ptr() + g * B * 4, value.data_ptr() + g * B * 4))
+        return rows
+
+    def launch(self, rows, tiles=None):
         tiles = self.tiles() if tiles is None else tiles
-        t = self.table(states, noise, out, tiles)
+        t = self.table(rows, tiles)
         check(self.L.hwy_ppo_group_act(ctypes.byref(self.dims), self.G,
                                        int(tiles[0] is not None), t.data_ptr(), stream_ptr()),
               "hwy_ppo_group_act")
 
+    def __call__(self, states, out, noise=None, tiles=None):
+        """All G agents on consecutive B-row blocks of one buffer set (see rows_of)."""
+        self.launch(self.rows_of(states, out, noise), tiles)
+
 
 class GroupStep:
-    """One minibatch step of G FusedPPO learners (same dims) in four launches
-    (hwy_ppo_group_step): learner g's arguments are its own FusedPPO._args, so each learner
-    steps bit for bit as its solo run() would.  One device table per minibatch index."""
+    """One minibatch step of G FusedPPO learners (same rows and hidden width; state dims may
+    differ) in four launches (hwy_ppo_group_step): learner g's arguments are its own
+    FusedPPO._args, so each learner steps bit for bit as its solo run() would.  One device table
+    (and plan) per minibatch index."""
 
     def __init__(self, fused):
         self.fused = list(fused)
         self.G = len(self.fused)
         F0 = self.fused[0]
-        self.L = F0.L
-        self.dims = F0.dims
-        nb = self.L.hwy_ppo_group_table_bytes(ctypes.byref(self.dims), self.G)
+        self.L = _bind_group(F0.L)
+        if any(F.mb != F0.mb or F.H != F0.H for F in self.fused):
+            raise ValueError("grouped PPO step: the learners share minibatch rows and hidden width")
+        nb = self.L.hwy_ppo_group_table_bytes(ctypes.byref(F0.dims), self.G)
         if nb < 0:
             raise ValueError(f"grouped PPO step: unsupported dims B={F0.mb} S={F0.S} H={F0.H} "
                              "(16-row tiles: minibatches below 8,192 rows)")
         self._nb = int(nb)
         self.tables: List[torch.Tensor] = []
+        self.plans: List[PpoGroupPlan] = []
 
     def prepare(self, per_learner_args) -> None:
         """per_learner_args[g][i]: learner g's PpoArgs of minibatch i."""
         nmb = len(per_learner_args[0])
-        self.tables = []
+        self.tables, self.plans = [], []
         for i in range(nmb):
             arr = (PpoArgs * self.G)()
             for g in range(self.G):
                 ctypes.memmove(ctypes.byref(arr[g]), ctypes.byref(per_learner_args[g][i]),
                                ctypes.sizeof(PpoArgs))
             t = torch.empty(self._nb, dtype=torch.uint8, device=self.fused[0].flat.device)
-            check(self.L.hwy_ppo_group_prepare(arr, self.G, t.data_ptr(), stream_ptr()),
-                  "hwy_ppo_group_prepare")
+            plan = PpoGroupPlan()
+            check(self.L.hwy_ppo_group_prepare(arr, self.G, t.data_ptr(), ctypes.byref(plan),
+                                               stream_ptr()), "hwy_ppo_group_prepare")
             self.tables.append(t)
+            self.plans.append(plan)
 
     def step(self, i: int) -> None:
-        check(self.L.hwy_ppo_group_step(ctypes.byref(self.dims), self.G, self.tables[i].data_ptr(),
+        check(self.L.hwy_ppo_group_step(ctypes.byref(self.plans[i]), self.tables[i].data_ptr(),
                                         stream_ptr()), "hwy_ppo_group_step")

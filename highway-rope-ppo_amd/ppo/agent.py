@@ -30,6 +30,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch.distributions import Normal
 
+from utils.graphs import capture as graph_capture
+
 METRIC_KEYS = ("policy_loss", "value_loss", "entropy", "loss", "clip_fraction", "approx_kl")
 _LOG_SQRT_2PI = 0.5 * math.log(2 * math.pi)
 
@@ -291,9 +293,9 @@ class _Learner:
                 self._opt()
         torch.cuda.current_stream().wait_stream(s)
         self.g_fwd, self.g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_fwd):
+        with graph_capture(self.g_fwd):
             self._fwd_bwd()
-        with torch.cuda.graph(self.g_opt):
+        with graph_capture(self.g_opt):
             self._opt()
 
     def step(self, idx: torch.Tensor):

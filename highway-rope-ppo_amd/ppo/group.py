@@ -22,9 +22,11 @@ kernels run the solo calls' bodies per learner, so each experiment is bit for bi
 
 from __future__ import annotations
 
-from typing import Callable, List, Optional, Sequence
+from typing import Callable, Optional, Sequence
 
 import torch
+
+from utils.graphs import capture as graph_capture
 
 from .agent import RolloutBuffer
 
@@ -69,7 +71,7 @@ class ExperimentGroup:
         self._roll_graph = None
         self._roll_key = None
         self._roll_seen = None
-        self._upd = None  # (key, GroupStep, graph)
+        self._upd = None  # the update's static inputs and argument structs (pre_update)
         self.iterations = 0
         # how the rollouts / updates were issued (graph replays vs eager runs vs captures, and
         # argument-table preparations): a sweep that keeps re-preparing shows here
@@ -88,63 +90,57 @@ class ExperimentGroup:
                         out=self._noise_tmp)
             buf.noise[:, g * E:(g + 1) * E].copy_(self._noise_tmp)
 
-    def _steps(self, tiles) -> None:
+    def act_rows(self, t: int, deterministic: bool = False):
+        """This group's acting rows at rollout step t (GroupAct.rows_of), or, deterministic, the
+        bootstrap row states[T] into the fixed bootstrap outputs."""
+        buf = self.buf
+        if deterministic:
+            return self.act.rows_of(buf.states[self.T], self._boot, None)
+        return self.act.rows_of(buf.states[t], (buf.actions[t], buf.pre_tanh[t], buf.log_probs[t],
+                                                buf.values[t]), buf.noise[t])
+
+    def env_step(self, t: int) -> None:
         buf, env = self.buf, self.env
-        GE = self.G * self.E
         obs_shape = env.obs_buf.shape[1:]
+        env.step_into(buf.actions[t], buf.states[t + 1].view(self.G * self.E, *obs_shape),
+                      buf.rewards[t], buf.terminated[t], buf.truncated[t], buf.ep_return[t],
+                      buf.ep_length[t])
+
+    def _steps(self, tiles) -> None:
         for t in range(self.T):
-            self.act(buf.states[t], (buf.actions[t], buf.pre_tanh[t], buf.log_probs[t],
-                                     buf.values[t]), noise=buf.noise[t], tiles=tiles)
-            env.step_into(buf.actions[t], buf.states[t + 1].view(GE, *obs_shape), buf.rewards[t],
-                          buf.terminated[t], buf.truncated[t], buf.ep_return[t],
-                          buf.ep_length[t])
-        buf.finish_dones()
+            self.act.launch(self.act_rows(t), tiles)
+            self.env_step(t)
+        self.buf.finish_dones()
 
     def rollout(self) -> None:
         """T steps of every experiment (LockstepRollout's order: act, then env step, per t);
         captured as one HIP graph once its launch arguments repeat."""
         self._draw_noise()
         tiles = self.act.tiles()  # also syncs acting-only tile images, outside any capture
-        if not self.use_graphs:
-            self._steps(tiles)
-            return
         key = (self.env._handle.value, self.env.launch_version, tuple(tiles))
-        if self._roll_graph is not None and key == self._roll_key:
-            self.stats["rollout_replay"] += 1
-            self._roll_graph.replay()
-            return
-        if key != self._roll_seen:  # first rollout at these arguments: eager (builds the tables)
-            self.stats["rollout_eager"] += 1
-            self._roll_seen = key
-            self._steps(tiles)
-            return
-        self.stats["rollout_capture"] += 1
-        g = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s):
-                self._steps(tiles)
-        torch.cuda.current_stream().wait_stream(s)
-        self._roll_graph, self._roll_key = g, key
-        g.replay()
+        self._roll_graph, self._roll_key, self._roll_seen = _graph_run(
+            self, self.use_graphs, key, lambda: self._steps(tiles), self._roll_graph,
+            self._roll_key, self._roll_seen, "rollout")
 
     # ------------------------------------------------------------------ update
     def bootstrap_values(self) -> torch.Tensor:
         """V(states[T]) of every experiment (PPOAgent.value: the deterministic act launch)."""
-        self.act(self.buf.states[self.T], self._boot, noise=None)
+        self.act.launch(self.act_rows(0, deterministic=True))
         return self._boot[3]
 
-    def update(self, return_metrics: bool = True):
-        """PPOAgent.update_rollout for every experiment at once (ppo/agent.py's batched update:
-        GAE, per-experiment advantage normalisation and permutation, epochs x minibatches of the
-        fused step, metrics)."""
+    def pre_update(self, last_values: torch.Tensor) -> dict:
+        """The update's inputs for every experiment, in its solo update_rollout's order on its
+        generator and samples (ppo/agent.py's batched update): GAE over the [T, G*E] rollout,
+        each experiment's advantage normalisation and permutation mapped into the grouped
+        rollout, the learners' FusedPPO (its Adam state handed over) with its per-update
+        refresh (counters, tile image).  Returns the context post_update and the step runner
+        use; ctx["args"][g][i] is learner g's PpoArgs of minibatch i, rebuilt only when the
+        buffers or hyper-parameters change (ctx["key"])."""
         from hwy import ops
-        from hwy.ppo_native import GroupStep
 
         buf, G, E, T = self.buf, self.G, self.E, self.T
         n, GE = T * E, G * E
-        adv, ret = ops.gae(buf.rewards, buf.dones, buf.values, self.bootstrap_values(),
+        adv, ret = ops.gae(buf.rewards, buf.dones, buf.values, last_values,
                            self.agents[0].gamma, self.agents[0].lam)
         sizes = self.agents[0].minibatch_sizes(n)
         mb, nmb = sizes[0], len(sizes)
@@ -157,21 +153,17 @@ class ExperimentGroup:
             F = ag._fused_for(mb, nmb, n)
             ag._adam_to("fused")
             fused.append(F)
-        if self._upd is None or self._upd[0] != (tuple(id(F) for F in fused), mb, nmb):
+        fkey = (tuple(id(F) for F in fused), mb, nmb)
+        if self._upd is None or self._upd[0] != fkey:
             # static inputs of the captured steps (FusedPPO's _static_bufs): advantages,
             # returns and the mapped permutations are copied in every update
-            adv_g = torch.empty(T * GE, device=self.dev)
-            ret_g = torch.empty(T * GE, device=self.dev)
-            idx = torch.empty(G, n, dtype=torch.int64, device=self.dev)
-            self._upd = [(tuple(id(F) for F in fused), mb, nmb), GroupStep(fused), None, adv_g,
-                         idx, None, ret_g]
-        _, step, graph, adv_grp, idx_all, bound, ret_flat = self._upd
+            self._upd = [fkey, torch.empty(T * GE, device=self.dev),
+                         torch.empty(T * GE, device=self.dev),
+                         torch.empty(G, n, dtype=torch.int64, device=self.dev),
+                         torch.empty(G, n, dtype=torch.int64, device=self.dev), None, None]
+        _, adv_grp, ret_flat, idx_all, perms, bound, args = self._upd
         adv3 = adv_grp.view(T, G, E)
-        perms = self._perms if getattr(self, "_perms", None) is not None else \
-            torch.empty(G, n, dtype=torch.int64, device=self.dev)
-        self._perms = perms
         for g, ag in enumerate(self.agents):
-            # the solo update_rollout's order on this experiment's generator and samples
             a = ag.normalize_advantages(adv[:, g * E:(g + 1) * E].reshape(n))
             adv3[:, g].copy_(a.view(T, E))
             torch.randperm(n, device=self.dev, generator=ag.generator, out=perms[g])
@@ -184,52 +176,39 @@ class ExperimentGroup:
         ret_flat.copy_(ret.reshape(T * GE))
         key = (states.data_ptr(), pre.data_ptr(), old_lp.data_ptr(), adv_grp.data_ptr(),
                ret_flat.data_ptr(), idx_all.data_ptr()) + tuple(F._scalar_key() for F in fused)
-        if bound != key:  # the learners' argument structs and the device tables, once per key
-            self.stats["update_prepare"] += 1
+        if bound != key:
             args = [[F._args(states, pre, old_lp, adv_grp, ret_flat,
                              idx_all[g].data_ptr() + i * mb * 8) for i in range(nmb)]
                     for g, F in enumerate(fused)]
-            step.prepare(args)
-            graph = None
-            self._upd[2] = None
-            self._upd[5] = key
-            self._args = args
-        args = self._args
+            self._upd[5], self._upd[6] = key, args
         for F, a in zip(fused, args):
             F._last_args, F._last_inputs = a, (states, pre, old_lp, adv_grp, ret_flat, idx_all)
             F.counters[1].zero_()
             F.sync_params(a[0])  # FusedPPO.run's tile-image refresh
-        epochs = self.agents[0].epochs
-        if not self.use_graphs:
-            for _ in range(epochs):
-                for i in range(nmb):
-                    step.step(i)
-        else:
-            if graph is None:  # one epoch's minibatch steps as one graph (FusedPPO._capture)
-                self.stats["update_capture"] += 1
-                graph = torch.cuda.CUDAGraph()
-                s = torch.cuda.Stream()
-                s.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(s):
-                    with torch.cuda.graph(graph, stream=s):
-                        for i in range(nmb):
-                            step.step(i)
-                torch.cuda.current_stream().wait_stream(s)
-                self._upd[2] = graph
-            for _ in range(epochs):
-                graph.replay()
+        return {"fused": fused, "args": args, "key": key, "sizes": sizes, "nmb": nmb, "ret": ret}
+
+    def post_update(self, ctx: dict, return_metrics=True):
+        buf, E, T = self.buf, self.E, self.T
+        n = T * E
         out = []
-        for g, (ag, F) in enumerate(zip(self.agents, fused)):
+        for g, (ag, F) in enumerate(zip(self.agents, ctx["fused"])):
             F._tiles_version = F._param_versions()
             ag.updates += 1
             if return_metrics:
                 vals = buf.values[:, g * E:(g + 1) * E].reshape(n)
-                rets = ret[:, g * E:(g + 1) * E].reshape(n)
-                out.append(ag._finish_metrics(F.metrics, sizes, vals, rets,
+                rets = ctx["ret"][:, g * E:(g + 1) * E].reshape(n)
+                out.append(ag._finish_metrics(F.metrics, ctx["sizes"], vals, rets,
                                               deferred=return_metrics == "deferred"))
         self.iterations += 1
         buf.states[0].copy_(buf.states[T])
         return out if return_metrics else None
+
+    def update(self, return_metrics: bool = True):
+        """PPOAgent.update_rollout for every experiment at once: pre_update, epochs x
+        minibatches of the grouped fused step (one graph per epoch), post_update."""
+        ctx = self.pre_update(self.bootstrap_values())
+        self._steps_runner = _run_group_steps(self, [ctx], getattr(self, "_steps_runner", None))
+        return self.post_update(ctx, return_metrics)
 
     def iteration(self, return_metrics=True):
         """One PPO iteration of every experiment: rollout, then update."""
@@ -251,6 +230,131 @@ class ExperimentGroup:
         d = self.buf.dones[:, g * E:(g + 1) * E]
         r = self.buf.ep_return[:, g * E:(g + 1) * E]
         return r[d != 0]
+
+
+def _graph_run(owner, use_graphs, key, steps, graph, gkey, seen, what):
+    """LockstepRollout's issue policy for a launch sequence `steps`: replay the captured graph
+    when its key repeats, run eagerly the first time a key is seen (allocations, argument
+    tables), capture it the second time.  Returns the new (graph, graph key, seen key)."""
+    if not use_graphs:
+        steps()
+        return graph, gkey, seen
+    if graph is not None and key == gkey:
+        owner.stats[f"{what}_replay"] += 1
+        graph.replay()
+        return graph, gkey, seen
+    if key != seen:
+        owner.stats[f"{what}_eager"] += 1
+        steps()
+        return graph, gkey, key
+    owner.stats[f"{what}_capture"] += 1
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with graph_capture(g, stream=s):
+            steps()
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    return g, key, seen
+
+
+def _run_group_steps(owner, ctxs, runner):
+    """Every epoch's minibatch steps of the learners of `ctxs` (pre_update contexts) as grouped
+    launches: one GroupStep over all of them, its tables prepared when any member's arguments
+    changed, one epoch captured as a graph and replayed `epochs` times (FusedPPO.run's
+    schedule).  runner = (key, GroupStep, graph) kept by the owner between updates."""
+    from hwy.ppo_native import GroupStep
+
+    fused = [F for c in ctxs for F in c["fused"]]
+    args = [a for c in ctxs for a in c["args"]]
+    key = (tuple(id(F) for F in fused),) + tuple(c["key"] for c in ctxs)
+    nmb = ctxs[0]["nmb"]
+    if any(c["nmb"] != nmb for c in ctxs):
+        raise ValueError("grouped learners need the same minibatch count")
+    if runner is None or runner[0] != key:
+        owner.stats["update_prepare"] += 1
+        step = GroupStep(fused)
+        step.prepare(args)
+        runner = (key, step, None)
+    _, step, graph = runner
+    epochs = fused[0].agent.epochs
+    if not owner.use_graphs:
+        for _ in range(epochs):
+            for i in range(nmb):
+                step.step(i)
+        return runner
+    if graph is None:  # one epoch's minibatch steps as one graph (FusedPPO._capture)
+        owner.stats["update_capture"] += 1
+        graph = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with graph_capture(graph, stream=s):
+                for i in range(nmb):
+                    step.step(i)
+        torch.cuda.current_stream().wait_stream(s)
+        runner = (key, step, graph)
+    for _ in range(epochs):
+        graph.replay()
+    return runner
+
+
+class GroupBatch:
+    """Several ExperimentGroups of one hidden width and the same rows per learner (a sweep's
+    cells that differ only in observation layout, e.g. the four h256 cells: no PE, RoPE, DistPE,
+    RankPE, whose state dims are 60 or 120) stepped as ONE set of launches: per rollout step one
+    acting launch for every learner of every group and each group's env step; per minibatch step
+    one grouped fused step over all their learners (hwy_ppo_group_step takes learners of
+    different state dims).  Each experiment stays bit-identical to its solo run: the same
+    kernel bodies per learner, each group's own generator order, GAE and normalisation."""
+
+    def __init__(self, groups, use_graphs: bool = True):
+        from hwy.ppo_native import GroupAct
+
+        self.groups = list(groups)
+        g0 = self.groups[0]
+        if any(g.E != g0.E or g.T != g0.T for g in self.groups):
+            raise ValueError("a batch's groups share envs per experiment and rollout length")
+        self.agents = [a for g in self.groups for a in g.agents]
+        self.act = GroupAct(self.agents, g0.E)
+        self.use_graphs = bool(use_graphs)
+        self.T = g0.T
+        self._roll = (None, None, None)
+        self._runner = None
+        self.stats = {"rollout_replay": 0, "rollout_eager": 0, "rollout_capture": 0,
+                      "update_prepare": 0, "update_capture": 0}
+
+    def _rows(self, t, deterministic=False):
+        return [r for g in self.groups for r in g.act_rows(t, deterministic)]
+
+    def _steps(self, tiles):
+        for t in range(self.T):
+            self.act.launch(self._rows(t), tiles)
+            for g in self.groups:
+                g.env_step(t)
+        for g in self.groups:
+            g.buf.finish_dones()
+
+    def rollout(self) -> None:
+        for g in self.groups:
+            g._draw_noise()
+        tiles = self.act.tiles()
+        key = (tuple((g.env._handle.value, g.env.launch_version) for g in self.groups),
+               tuple(tiles))
+        self._roll = _graph_run(self, self.use_graphs, key, lambda: self._steps(tiles), *self._roll,
+                                "rollout")
+
+    def update(self, return_metrics=True):
+        self.act.launch(self._rows(0, deterministic=True))  # every group's bootstrap values
+        ctxs = [g.pre_update(g._boot[3]) for g in self.groups]
+        self._runner = _run_group_steps(self, ctxs, self._runner)
+        return [g.post_update(c, return_metrics) for g, c in zip(self.groups, ctxs)]
+
+    def iteration(self, return_metrics=True):
+        """One PPO iteration of every experiment of every group: a list per group."""
+        self.rollout()
+        return self.update(return_metrics)
 
 
 def build_group(condition, base_config, seeds: Sequence[int], envs_per_experiment: int,

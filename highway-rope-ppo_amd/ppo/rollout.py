@@ -17,6 +17,8 @@ from typing import Optional
 
 import torch
 
+from utils.graphs import capture as graph_capture
+
 
 class LockstepRollout:
     def __init__(self, agent, env, buf, use_graph: bool = True):
@@ -70,7 +72,7 @@ class LockstepRollout:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s):
+            with graph_capture(g, stream=s):
                 self._steps()
         torch.cuda.current_stream().wait_stream(s)
         self._graph, self._key = g, key

@@ -109,8 +109,8 @@ typedef struct hwy_ppo_act_args {
 } hwy_ppo_act_args;
 int hwy_ppo_act(const hwy_ppo_act_args* a, void* stream);
 
-/* ---- Grouped learners: G independent learners of the same dims (a sweep's seeds of one
- * condition, experiments/sweep.py; the reference runs them as separate processes,
+/* ---- Grouped learners: G independent learners (a sweep cell's seeds, or the cells of one
+ * hidden width; ppo/group.py, ExperimentRunner.launch_group; the reference runs them as separate processes,
  * experiments/runner.py:46-155 under main.py:188-242's joblib / SLURM fan-out) stepped in ONE
  * launch per kernel.  Workgroup (x, y) runs the solo launch's workgroup x for learner y, whose
  * kernel arguments the kernels read from a device table; the kernel bodies and tile shapes are
@@ -120,12 +120,21 @@ int hwy_ppo_act(const hwy_ppo_act_args* a, void* stream);
  *
  * hwy_ppo_group_step = hwy_ppo_forward_backward + hwy_ppo_optimizer for every learner (fused
  * path with 16-row tiles, i.e. minibatches below 64 x CUs rows; grads_modified == 0; 16-byte
- * aligned flat buffers).  -1 bad arguments / unsupported dims, -2 HIP error. */
+ * aligned flat buffers).  The learners share B and H; their state dims S may differ (e.g. the
+ * h256 cells of a sweep: no PE S = N*F, RankPE / DistPE S = N*(F+d)): each launch covers the
+ * largest learner's grid (the plan prepare writes) and a learner's surplus workgroups exit.
+ * hwy_ppo_group_table_bytes depends on B, H and G only.  -1 bad arguments / unsupported dims,
+ * -2 HIP error. */
+typedef struct hwy_ppo_group_plan {
+  int32_t G, B, H;                                    /* learners; shared minibatch rows, hidden */
+  int32_t grid_rows, grid_wgrad, grid_wsum, grid_adam; /* each launch's grid: the largest learner's */
+} hwy_ppo_group_plan;
 int64_t hwy_ppo_group_table_bytes(const hwy_ppo_dims* d, int G);
-int hwy_ppo_group_prepare(const hwy_ppo_args* a /*[G]*/, int G, void* table, void* stream);
-int hwy_ppo_group_step(const hwy_ppo_dims* d, int G, const void* table, void* stream);
-/* hwy_ppo_act for G learners; `tiles` = whether the learners' args carry tile images (all or
- * none), which picks the solo call's kernel. */
+int hwy_ppo_group_prepare(const hwy_ppo_args* a /*[G]*/, int G, void* table,
+                          hwy_ppo_group_plan* plan, void* stream);
+int hwy_ppo_group_step(const hwy_ppo_group_plan* plan, const void* table, void* stream);
+/* hwy_ppo_act for G learners (same B and H; S may differ); `tiles` = whether the learners' args
+ * carry tile images (all or none), which picks the solo call's kernel. */
 int64_t hwy_ppo_group_act_table_bytes(int G);
 int hwy_ppo_group_act_prepare(const hwy_ppo_act_args* a /*[G]*/, int G, void* table, void* stream);
 int hwy_ppo_group_act(const hwy_ppo_dims* d, int G, int tiles, const void* table, void* stream);

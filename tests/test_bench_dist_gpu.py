@@ -34,7 +34,7 @@ def test_bench_two_ranks_one_line():
     assert len(lines) == 1
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["cpu_baseline"] is None
-    assert d["config"]["global_envs"] == 512 and d["roofline"]["includes_allreduce"] is True
+    assert d["config"]["global_envs"] == 512
     assert abs(d["value"] - 512 * 8 * 2 / (d["ms_per_step"] * 2e-3)) / d["value"] < 0.01
     # the all-reduce's own cost beside the step it burdens: the flat gradient
     # bucket of ActorCritic(60, 2, 256) in fp32, timed alone, and the step time that includes it
@@ -43,18 +43,16 @@ def test_bench_two_ranks_one_line():
     n_params = S * H + H + 3 * (H * H + H) + 2 * H + 2 + 2 + H + 1
     ar = roof["allreduce"]
     assert ar["bytes"] == 4 * n_params and ar["us_per_allreduce"] > 0
-    # the event time spans the all-reduce in either capture mode the update may run in, so the
-    # share of one all-reduce in the step that includes it lies in (0, 1); the printed share is
-    # re-derived from the printed (rounded) fields at a relative tolerance, never bit-equal
-    assert d["config"]["epoch_graph_collectives"] in ("captured",
-                                                      "per-step graphs, all-reduce between them")
-    assert roof["step_us_with_allreduce"] == roof["avg_launch_us"] > 0
+    # gloo cannot be captured: the all-reduce runs host-mediated between per-step graphs, where
+    # the epoch events do not span it (bench.py), so the step that includes it is the
+    # synchronised update's host clock per step; one all-reduce is a share of it in (0, 1), and
+    # the printed share is re-derived from the printed (rounded) fields at rel 1e-3
+    assert d["config"]["epoch_graph_collectives"] == "per-step graphs, all-reduce between them"
+    assert roof["includes_allreduce"] is False
+    assert roof["step_us_with_allreduce"] == roof["update_host_us_per_step"] > 0
     share = roof["allreduce_share_of_step"]
-    assert share == pytest.approx(ar["us_per_allreduce"] / roof["avg_launch_us"], rel=1e-3)
-    assert 0 < share < 1, (share, ar, roof["avg_launch_us"], roof["update_host_us_per_step"])
-    # the host clock of a synchronised update agrees with the event time (the host clock also
-    # holds the launches' host overhead, so it may run longer, never much shorter)
-    assert 0.5 < roof["update_host_us_per_step"] / roof["avg_launch_us"] < 4.0
+    assert share == pytest.approx(ar["us_per_allreduce"] / roof["step_us_with_allreduce"], rel=1e-3)
+    assert 0 < share < 1, (share, ar, roof["step_us_with_allreduce"], roof["avg_launch_us"])
     # the line proves its ranks from the communicator: world size and backend
     # as the process group reports them, every rank's device and PCI location, whether the epoch
     # graph captured the collective; gloo rehearses both ranks on one GPU (one distinct device)

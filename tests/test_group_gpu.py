@@ -90,6 +90,46 @@ def test_group_matches_solo_runs_bit_for_bit(cond_name, d, H, order):
     assert grp.episode_returns(0).numel() == int(grp.buf.dones[:, :E].sum())
 
 
+def test_group_batch_of_cells_with_different_state_dims_matches_solo_runs():
+    """GroupBatch: two h256 cells whose learners differ in state dim (sorted, S 60; shuffled
+    RankPE d_embed 4, S 120) stepped as one set of launches -- one acting launch per step over
+    both cells' learners, one grouped minibatch step whose grids cover the larger learner --
+    and every experiment still equals its solo run bit for bit."""
+    from config.base_config import HIGHWAY_CONFIG
+    from experiments.config import Condition
+    from ppo.agent import PPOAgent
+    from ppo.group import GroupBatch, build_group
+
+    E, T, iters = 16, 16, 3
+    cells = [(Condition.SORTED, None, [42, 1042]), (Condition.SHUFFLED_RANKPE, 4, [7, 2042, 99])]
+    groups = [build_group(c, HIGHWAY_CONFIG, seeds, E, T, DEV,
+                          lambda sd: PPOAgent(sd, 2, device=DEV, **_hp(256)), d_embed=d)
+              for c, d, seeds in cells]
+    assert {g.sd for g in groups} == {60, 120}
+    batch = GroupBatch(groups)
+    hist = []
+    for _ in range(iters):
+        batch.rollout()
+        hist.append([{k: getattr(g.buf, k).clone() for k in ("states", "rewards", "log_probs")}
+                     for g in groups])
+        batch.update()
+    torch.cuda.synchronize()
+    for gi, (c, d, seeds) in enumerate(cells):
+        for j, s in enumerate(seeds):
+            agent, shist, _, env = _solo(c, d, s, E, T, iters, 256, {})
+            sl = slice(j * E, (j + 1) * E)
+            for it in range(iters):
+                for k, v in hist[it][gi].items():
+                    assert torch.equal(v[:, sl], shist[it][k]), (gi, j, it, k)
+            for (k, va), (_, vb) in zip(agent.actor_critic.state_dict().items(),
+                                        groups[gi].agents[j].actor_critic.state_dict().items()):
+                assert torch.equal(va, vb), (gi, j, k)
+            env.close()
+    # one argument-table preparation for the whole batch; the third rollout (the second at the
+    # updated weights' tile images) was captured as a graph
+    assert batch.stats["update_prepare"] == 1 and batch.stats["rollout_capture"] == 1
+
+
 def test_group_env_seeds_follow_each_experiments_schedule():
     """hwy_set_seed_groups: group g's envs reset with seed_bases[g] + l + 1 (+ E per episode),
     so a grouped handle's first observations equal each solo handle's."""
