@@ -37,13 +37,26 @@ constexpr int kSlice = 64 * 64;   // floats per published slice (16 KB)
 constexpr int kPhases = 6;        // work phases per tile; kPhases - 1 seams
 constexpr int kPollCap = 400000;
 
+// The s_nop: a VALU write to the data registers of a store wider than 8 bytes needs one wait
+// state after the store, and the compiler's hazard recognizer does not look inside this asm (the
+// first build overwrote v[34:37] right after the store: 12.5 % of the words arrived corrupted).
 __device__ __forceinline__ void store_wt(float* p, f32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
-__device__ __forceinline__ f32x4 load_wt(const float* p) {
-  f32x4 r;
-  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(r) : "v"(p) : "memory");
-  return r;
+// six write-through loads in flight, then one wait: a single asm statement, so the compiler cannot
+// touch a destination register before the loads have landed
+__device__ __forceinline__ void load6_wt(f32x4 (&v)[6], const float* const (&p)[6]) {
+  asm volatile(
+      "global_load_dwordx4 %0, %6, off sc1\n"
+      "global_load_dwordx4 %1, %7, off sc1\n"
+      "global_load_dwordx4 %2, %8, off sc1\n"
+      "global_load_dwordx4 %3, %9, off sc1\n"
+      "global_load_dwordx4 %4, %10, off sc1\n"
+      "global_load_dwordx4 %5, %11, off sc1\n"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5])
+      : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5])
+      : "memory");
 }
 __device__ __forceinline__ float tagval(int cluster, int member, int seam, int launch, int i) {
   return (float)(((cluster * 7 + member * 3 + seam * 11 + launch * 13) & 1023) * 4096 + (i & 4095));
@@ -52,7 +65,8 @@ __device__ __forceinline__ float tagval(int cluster, int member, int seam, int l
 template <int SEAMS>
 __global__ void __launch_bounds__(64 * kNW) cluster_tile(const float* __restrict__ w,
                                                          float* slab, int* counters, int* err,
-                                                         float* out, int W, int launch) {
+                                                         float* out, int W, int launch,
+                                                         int* wg_xcc, int* wg_bad) {
   const int b = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int cluster = (b & 7) + 8 * ((b >> 3) / kK), member = (b >> 3) % kK;
   const int nclusters = gridDim.x / kK;
@@ -115,13 +129,14 @@ __global__ void __launch_bounds__(64 * kNW) cluster_tile(const float* __restrict
     __syncthreads();
     // read the three peer slices: 96 B per thread, write-through loads
     f32x4 v[6];
+    const float* p[6];
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
       const int peer = (member + 1 + q / 2) % kK;
       const int i = ((q & 1) * 64 * kNW + threadIdx.x) * 4;
-      v[q] = load_wt(slab + ((size_t)(seam * nclusters + cluster) * kK + peer) * kSlice + i);
+      p[q] = slab + ((size_t)(seam * nclusters + cluster) * kK + peer) * kSlice + i;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    load6_wt(v, p);
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
       const int peer = (member + 1 + q / 2) % kK;
@@ -135,11 +150,15 @@ __global__ void __launch_bounds__(64 * kNW) cluster_tile(const float* __restrict
     a[0] += check * 1e-30f;
   }
   if (bad && !s_timeout) atomicAdd(err, bad);
+  if (threadIdx.x == 0) wg_xcc[b] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
+  if (bad) atomicAdd(wg_bad + b, bad);
   float s = check;
 #pragma unroll
   for (int r = 0; r < 4; ++r) s += acc[r][0] + acc[r][1] + acc[r][2] + acc[r][3];
   out[b * blockDim.x + threadIdx.x] = s;
 }
+
+int *g_xcc, *g_bad;
 
 template <int SEAMS>
 float run(const char* name, int W, const float* w, float* slab, int* counters, int* err,
@@ -149,14 +168,15 @@ float run(const char* name, int W, const float* w, float* slab, int* counters, i
   hipEventCreate(&e1);
   hipMemset(counters, 0, 64 * sizeof(int) * 4);
   hipMemset(err, 0, 2 * sizeof(int));
+  hipMemset(g_bad, 0, 256 * sizeof(int));
   launch = 0;
   for (int i = 0; i < 3; ++i, ++launch)  // warm-up
     hipLaunchKernelGGL(cluster_tile<SEAMS>, dim3(256), dim3(64 * kNW), 0, 0, w, slab, counters, err,
-                       out, W, launch);
+                       out, W, launch, g_xcc, g_bad);
   hipEventRecord(e0);
   for (int i = 0; i < reps; ++i, ++launch)
     hipLaunchKernelGGL(cluster_tile<SEAMS>, dim3(256), dim3(64 * kNW), 0, 0, w, slab, counters, err,
-                       out, W, launch);
+                       out, W, launch, g_xcc, g_bad);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms = 0;
@@ -164,6 +184,25 @@ float run(const char* name, int W, const float* w, float* slab, int* counters, i
   int herr[2];
   hipMemcpy(herr, err, sizeof(herr), hipMemcpyDeviceToHost);
   const float us = ms * 1e3f / reps;
+  if (herr[0]) {  // which workgroups read stale words: by XCC of the cluster's members
+    int xcc[256], bad[256];
+    hipMemcpy(xcc, g_xcc, sizeof(xcc), hipMemcpyDeviceToHost);
+    hipMemcpy(bad, g_bad, sizeof(bad), hipMemcpyDeviceToHost);
+    int split = 0, split_bad = 0, same_bad = 0, nbad = 0;
+    for (int c = 0; c < 64; ++c) {
+      int m[4], any = 0;
+      for (int j = 0; j < 4; ++j) m[j] = (c & 7) + 8 * (4 * (c >> 3) + j);
+      const bool same = xcc[m[0]] == xcc[m[1]] && xcc[m[0]] == xcc[m[2]] && xcc[m[0]] == xcc[m[3]];
+      for (int j = 0; j < 4; ++j) any += bad[m[j]], nbad += bad[m[j]] > 0;
+      split += !same;
+      if (same) same_bad += any; else split_bad += any;
+    }
+    printf("    clusters spanning XCCs %d/64; stale words in them %d, in single-XCC clusters %d; workgroups with stale reads %d/256\n",
+           split, split_bad, same_bad, nbad);
+    printf("    xcc of blocks 0..15:");
+    for (int i = 0; i < 16; ++i) printf(" %d", xcc[i]);
+    printf("\n");
+  }
   printf("%-22s W %3d blocks/wave/phase: %8.2f us per launch  (mismatched words %d, poll timeouts %d)\n",
          name, W, us, herr[0], herr[1]);
   hipEventDestroy(e0);
@@ -185,6 +224,8 @@ int main() {
   hipMalloc(&slab, (size_t)(kPhases - 1) * 64 * kK * kSlice * 4);
   hipMalloc(&counters, 64 * sizeof(int) * 4);
   hipMalloc(&err, 2 * sizeof(int));
+  hipMalloc(&g_xcc, 256 * sizeof(int));
+  hipMalloc(&g_bad, 256 * sizeof(int));
   hipMalloc(&out, 256 * 64 * kNW * 4);
   int launch = 0;
   const int reps = 200;
