@@ -71,14 +71,15 @@ def test_metric_string_is_baselines():
 def test_per_kernel_roofline_reproduces_from_the_cited_rocprof_file():
     """The line's per-kernel roofline from the committed rocprofv3 summary of its workload
     (bench.rocprof_per_kernel): the four kernels parse, and their summed
-    durations reproduce the committed default line's epoch-event step time within 2 %."""
+    durations reproduce, within 2 %, the epoch-event step time that the same profiled command
+    printed (bench_prof_c1.json: the bench line of the rocprofv3 run the summary comes from)."""
     import json
     import os
 
     import bench
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    line = json.loads(open(os.path.join(root, "profiles", "r5", "measure", "bench_c1.json"))
+    line = json.loads(open(os.path.join(root, "profiles", "r6", "measure", "bench_prof_c1.json"))
                       .read().strip().splitlines()[-1])
     roof = line["roofline"]
     kf = bench.ppo_kernel_flops_per_sample(60, 256)
