@@ -17,6 +17,7 @@ reproduce them exactly.  Also writes OUT/sweep.json (wall time, per-cell agreeme
 one line per cell.
 
     python tools/sweep_reward.py --out gpurun_out/sweep_reward [--cells sorted_h256 ...]
+        [--seeds 42 1042 ...] [--work /tmp/sweep_work]
 """
 
 from __future__ import annotations
@@ -40,6 +41,10 @@ CELLS = {"sorted_h256": ("sorted", 256), "sorted_h384": ("sorted", 384),
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--out", default="gpurun_out/sweep_reward")
+    p.add_argument("--work", default=None,
+                   help="where the runner writes each cell's logs, checkpoints and artifacts "
+                        "(default: the cell's directory under --out); the summaries always go "
+                        "under --out")
     p.add_argument("--cells", nargs="+", default=list(CELLS))
     p.add_argument("--seeds", type=int, nargs="+", default=[42 + 1000 * k for k in range(10)])
     p.add_argument("--episodes", type=int, default=1500)
@@ -84,8 +89,11 @@ def main():
                                    env_config_overrides={}))
         run_dir = os.path.join(out, f"{cname}_h{H}_e{E}_t{T}")  # tools/condition_order.py layout
         os.makedirs(run_dir, exist_ok=True)
+        work_dir = (run_dir if args.work is None
+                    else os.path.join(os.path.abspath(args.work), os.path.basename(run_dir)))
+        os.makedirs(work_dir, exist_ok=True)
         cwd = os.getcwd()
-        os.chdir(run_dir)
+        os.chdir(work_dir)
         t0 = time.time()
         try:
             results = ExperimentRunner(HIGHWAY_CONFIG).launch_group(exps)
