@@ -124,8 +124,11 @@ def main():
                     row.update(final_reward=round(float(avg[-1]), 4),
                                max_reward=round(float(max(avg)), 4),
                                evals=[round(float(x), 2) for x in hist.get("eval_rewards", [])],
+                               eval_episodes=[int(x) for x in hist.get("eval_episode_numbers", [])],
                                env_steps=int(sum(u.get("steps", 0) for u in ups)),
-                               updates=len(ups))
+                               updates=len(ups),
+                               # the group's wall clock, shared by its experiments
+                               wall_s=round(wall, 1), train_s=round(wall, 1))
                     if e.seed in ref:
                         row.update(reference_final_reward=ref[e.seed],
                                    delta=round(row["final_reward"] - ref[e.seed], 4))
