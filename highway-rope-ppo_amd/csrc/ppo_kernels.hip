@@ -834,11 +834,6 @@ __device__ __forceinline__ int row_pitch(int n) { return lds_pitch(n); }
 // to the padded K).
 #define H_TW(QH, NW) ((64 * (QH)) / (NW) / 16)
 
-#ifndef HWY_ROWS_STAGE
-#define HWY_ROWS_STAGE 0
-#endif
-constexpr int kRowsStage = HWY_ROWS_STAGE;  // WRing KS of the 16-row H 256 row kernel
-
 struct WSeg {
   const float* W;
   int ldw, K, nblk, nn;  // nn: 0 W is [N][K], 1 W is [K][N] (k-major), 2 W is a tile image
@@ -847,20 +842,11 @@ struct WSeg {
 // UNI: the tile-image block address is made wave-uniform (scalar base + one 32-bit lane offset);
 // it frees the VGPRs the compact ppo_rows needs to fit two workgroups per CU (141 -> 134 us at
 // 16,384 rows) but costs the 16-row kernels at H 384 (648 -> 686 us at 32,768 rows, S 240)
-// KS (staging, 16-row ppo_rows at H 256): segments 1 (W2, forward) and 4 (Wa1, backward) take
-// their blocks D .. D + KS - 1 from stg, loaded by stage<SEG>() in a window where the weight
-// stream would idle -- the states gather before layer 1, the loss head before dh2 -- instead of
-// from the ring; the ring skips them.  The blocks are consumed in the same order (same bits).
-template <int TW, int D, int NSEG, bool TL, bool UNI = false, int KS = 0>
+template <int TW, int D, int NSEG, bool TL, bool UNI = false>
 struct WRing {
   f32x4 buf[D][TW];
-  f32x4 stg[KS > 0 ? KS : 1][TW];
   WSeg sg[NSEG];
   int n_base, g, c;
-  static_assert(KS % D == 0, "staged blocks: whole ring rounds");
-  static constexpr bool gap(int s) { return KS > 0 && (s == 1 || s == 4); }
-  // blocks of segment s the ring streams (the staged ones excluded)
-  __device__ __forceinline__ int nvis(int s) const { return sg[s].nblk - (gap(s) ? KS : 0); }
 
   // Branch-free loads (so the compiler can count them): element (k, n) of segment s sits at
   // W + n*sn + k*sk with (sn, sk) = (ldw, 1) for [N][K] and (1, ldw) for [K][N]; k past K is
@@ -897,18 +883,12 @@ struct WRing {
   template <int SEG>
   __device__ __forceinline__ void load_ahead(int b, f32x4 (&dst)[TW]) {
     constexpr int NX = SEG + 1 < NSEG ? SEG + 1 : SEG;
-    const int n0 = nvis(SEG);
-    const bool nxt = b >= n0;
+    const bool nxt = b >= sg[SEG].nblk;
     const WSeg& s0 = sg[SEG];
     const WSeg& s1 = sg[NX];
     const float* W = nxt ? s1.W : s0.W;
     const int ldw = nxt ? s1.ldw : s0.ldw, nn = nxt ? s1.nn : s0.nn, K = nxt ? s1.K : s0.K;
-    int j = nxt ? b - n0 : b;  // block of the segment in ring order
-    if constexpr (gap(SEG) || gap(NX)) {
-      const bool gp = nxt ? gap(NX) : gap(SEG);
-      if (gp && j >= D) j += KS;  // past the staged blocks
-    }
-    int kb = 16 * j;
+    int kb = nxt ? 16 * (b - s0.nblk) : 16 * b;
     if (SEG + 1 >= NSEG && nxt) kb = 0;
     // k + 3 < K for every lane (K % 4 == 0); a tile image holds whole (zero-padded) blocks, so
     // its block index stays wave-uniform
@@ -919,17 +899,6 @@ struct WRing {
 #pragma unroll
     for (int d = 0; d < D; ++d) load_ahead<0>(d, buf[d]);
     __builtin_amdgcn_sched_barrier(0);
-  }
-  // load segment SEG's staged blocks D .. D + KS - 1 into stg (their registers must be free:
-  // the previous staged segment consumed)
-  template <int SEG>
-  __device__ __forceinline__ void stage() {
-    if constexpr (gap(SEG)) {
-      const WSeg& s0 = sg[SEG];
-#pragma unroll
-      for (int i = 0; i < KS; ++i) load_blk(s0.W, s0.ldw, s0.nn, 16 * (D + i), stg[i]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
   }
   // acc += act[16 RB][16*nblk] (LDS, pitch pa) x segment SEG's weights for this wave's columns;
   // the RB 16-row blocks share every weight register block (RB = 2 halves the weight stream
@@ -942,73 +911,34 @@ struct WRing {
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
       a_nxt[rb] = *reinterpret_cast<const f32x4*>(arow + 16 * rb * pa);
-    // block kb / 16 of the segment with weights w; refill >= 0: the ring slot's next block (in
-    // ring order) goes out after the MFMAs (the same steps as the loop without staging below)
-    auto blk = [&](int kb, const f32x4 (&w)[TW], f32x4 (&slot)[TW], int refill) {
-      f32x4 a[RB];  // activations of this block, read one block ahead
-      const int kn = min(kb + 16, 16 * (nblk - 1));
+    for (int b0 = 0; b0 < nblk; b0 += D) {
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb) {
-        a[rb] = a_nxt[rb];
-        a_nxt[rb] = *reinterpret_cast<const f32x4*>(arow + 16 * rb * pa + kn);
-      }
-      // pinned: the next block's activation reads go out before this block's MFMAs (the
-      // scheduler otherwise sinks them to the block's end, right before their use)
-      __builtin_amdgcn_sched_barrier(0);
-      const bool kin = kb + 4 * g < sg[SEG].K;  // else the block was clamped: weights are 0
+      for (int d = 0; d < D; ++d) {
+        const int kb = 16 * (b0 + d);
+        f32x4 a[RB];  // activations of this block, read one block ahead
+        const int kn = min(kb + 16, 16 * (nblk - 1));
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int t = 0; t < TW; ++t) {
-          const float bw = kin ? w[t][j] : 0.0f;
-#pragma unroll
-          for (int rb = 0; rb < RB; ++rb)
-            acc[rb][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rb][j], bw, acc[rb][t], 0, 0, 0);
+        for (int rb = 0; rb < RB; ++rb) {
+          a[rb] = a_nxt[rb];
+          a_nxt[rb] = *reinterpret_cast<const f32x4*>(arow + 16 * rb * pa + kn);
         }
-      // issue the refill here: the scheduler would otherwise sink it next to its use
-      __builtin_amdgcn_sched_barrier(0);
-      if (refill >= 0) load_ahead<SEG>(refill, slot);
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    if constexpr (gap(SEG)) {
-      // ring blocks 0 .. D-1, the staged D .. D+KS-1, then the ring from D+KS on (ring order:
-      // block b >= D+KS is ring block b - KS)
+        // pinned: the next block's activation reads go out before this block's MFMAs (the
+        // scheduler otherwise sinks them to the block's end, right before their use)
+        __builtin_amdgcn_sched_barrier(0);
+        const bool kin = kb + 4 * g < sg[SEG].K;  // else the block was clamped: weights are 0
 #pragma unroll
-      for (int d = 0; d < D; ++d) blk(16 * d, buf[d], buf[d], d + D);
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int i = 0; i < KS; ++i) blk(16 * (D + i), stg[i], stg[i], -1);
-      for (int b0 = D + KS; b0 < nblk; b0 += D) {
+          for (int t = 0; t < TW; ++t) {
+            const float bw = kin ? buf[d][t][j] : 0.0f;
 #pragma unroll
-        for (int d = 0; d < D; ++d) blk(16 * (b0 + d), buf[d], buf[d], b0 - KS + d + D);
-      }
-    } else {
-      for (int b0 = 0; b0 < nblk; b0 += D) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-          const int kb = 16 * (b0 + d);
-          f32x4 a[RB];  // activations of this block, read one block ahead
-          const int kn = min(kb + 16, 16 * (nblk - 1));
-#pragma unroll
-          for (int rb = 0; rb < RB; ++rb) {
-            a[rb] = a_nxt[rb];
-            a_nxt[rb] = *reinterpret_cast<const f32x4*>(arow + 16 * rb * pa + kn);
+            for (int rb = 0; rb < RB; ++rb)
+              acc[rb][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rb][j], bw, acc[rb][t], 0, 0, 0);
           }
-          __builtin_amdgcn_sched_barrier(0);
-          const bool kin = kb + 4 * g < sg[SEG].K;
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int t = 0; t < TW; ++t) {
-              const float bw = kin ? buf[d][t][j] : 0.0f;
-#pragma unroll
-              for (int rb = 0; rb < RB; ++rb)
-                acc[rb][t] =
-                    __builtin_amdgcn_mfma_f32_16x16x4f32(a[rb][j], bw, acc[rb][t], 0, 0, 0);
-            }
-          __builtin_amdgcn_sched_barrier(0);
-          load_ahead<SEG>(b0 + d + D, buf[d]);
-          __builtin_amdgcn_sched_barrier(0);
-        }
+        // issue the refill here: the scheduler would otherwise sink it next to its use
+        __builtin_amdgcn_sched_barrier(0);
+        load_ahead<SEG>(b0 + d + D, buf[d]);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
@@ -1028,8 +958,8 @@ constexpr int ring_depth() { return TW <= 4 ? 4 : 2; }
 // segment table of the row kernels: forward W1, W2, Wa1, Wc1 ([N][K]); backward Wa1, Wc1, W2
 // read k-major for dh2 = dac [Wa1; Wc1] and dh1 = dh2 W2.  With a tile image (TileGeom; kept by
 // hwy_ppo_sync_params / ppo_adam) every segment streams whole 1-KB tiles instead.
-template <int TW, int D, int NSEG, bool TL, bool UNI, int KS>
-__device__ __forceinline__ void ring_setup(WRing<TW, D, NSEG, TL, UNI, KS>& R, const float* P,
+template <int TW, int D, int NSEG, bool TL, bool UNI>
+__device__ __forceinline__ void ring_setup(WRing<TW, D, NSEG, TL, UNI>& R, const float* P,
                                            const int64_t* off, int S, int H, int n_base,
                                            const float* tiles) {
   const int lane = threadIdx.x & 63;
@@ -1223,8 +1153,8 @@ __device__ __forceinline__ void gather_issue(const float* states, const int64_t*
 // MSK: the ReLU decisions of h1 and h2 (this lane's C elements) also go to mb[0], mb[1] as bits
 // (row_epi_bias_relu_bits), so the backward needs neither image for its masks.
 template <int QH, int NW, int RT, bool KEEP, int D, int NSEG, bool TL, bool MSK = false,
-          bool UNI = false, int KS = 0>
-__device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG, TL, UNI, KS>& R,
+          bool UNI = false>
+__device__ __forceinline__ void rows_forward(WRing<H_TW(QH, NW), D, NSEG, TL, UNI>& R,
                                              const float* states,
                                              const int64_t* idx, int S, int nrows, int row0,
                                              const float* P, const int64_t* off, float* X,
@@ -1366,9 +1296,7 @@ __device__ __forceinline__ void rows_body(const RowArgs& r) {
   const int nrows = min(RT, r.B - row0);
   const float* P = r.params;
   constexpr int D = CMP ? kRingDC : ring_depth<TW>();  // CMP: 4 waves per SIMD hide more
-  // staged weight blocks (WRing KS) at 16-row tiles, H 256: 8 per wave, 64 VGPRs
-  constexpr int KS = (!CMP && QH == 4 && RT == 16) ? kRowsStage : 0;
-  WRing<TW, D, 7, true, CMP, KS> R;
+  WRing<TW, D, 7, true, CMP> R;
   ring_setup(R, P, r.off, S, H, w * (H / NW), r.tiles);
   // the loss head's inputs and weights, loaded now so that their latency hides behind the
   // forward: lane l < RPW of wave w holds row RPW*w + l; the head weights of this wave's
@@ -1386,7 +1314,6 @@ __device__ __forceinline__ void rows_body(const RowArgs& r) {
   hadv = r.adv[hsrc];
   hret = r.ret[hsrc];
   R.prime();
-  R.template stage<1>();  // W2's blocks D .. D+KS-1, under the gather
   const int nb = w * (H / NW);  // this wave's output columns of an H-wide layer
   f32x4 acc[RB][TW];
   // the squash correction depends on the stored pre-tanh actions only: computed here, its
@@ -1414,7 +1341,6 @@ __device__ __forceinline__ void rows_body(const RowArgs& r) {
                                                   H1, P1, AC, r.xg, r.h1,
                                                   r.h2, mb, av,
                                                   cv PSEC_ARGS, &xpre);
-  R.template stage<4>();  // Wa1's backward blocks D .. D+KS-1, under the loss head
   PSEC(3);
   const int g4 = lane >> 4, c16 = lane & 15;
 
