@@ -184,3 +184,36 @@ def test_runner_launch_group_equals_launch(tmp_path, monkeypatch):
         assert mg["eval_episode_numbers"] == ms["eval_episode_numbers"]
         assert [u["loss"] for u in mg["policy_updates"]] == [u["loss"] for u in ms["policy_updates"]]
     assert (tmp_path / "artifacts").exists() or any(tmp_path.iterdir())
+
+
+def test_group_eager_equals_graph_replay():
+    """use_graphs=False (every rollout step and minibatch step launched eagerly) and the default
+    graph capture / replay give the same experiments bit for bit."""
+    from config.base_config import HIGHWAY_CONFIG
+    from experiments.config import Condition
+    from ppo.agent import PPOAgent
+    from ppo.group import build_group
+
+    E, T, iters, seeds = 16, 16, 3, [42, 1042]
+    out = []
+    for graphs in (True, False):
+        grp = build_group(Condition.SHUFFLED_DISTPE, HIGHWAY_CONFIG, seeds, E, T, DEV,
+                          lambda sd: PPOAgent(sd, 2, device=DEV, **_hp(256)), d_embed=4,
+                          use_graphs=graphs)
+        hist = []
+        for _ in range(iters):
+            grp.rollout()
+            hist.append({k: getattr(grp.buf, k).clone() for k in ("states", "log_probs", "values")})
+            hist[-1]["metrics"] = grp.update()
+        torch.cuda.synchronize()
+        w = [torch.cat([p.detach().reshape(-1) for p in ag.actor_critic.parameters()]).clone()
+             for ag in grp.agents]
+        out.append((hist, w, dict(grp.stats)))
+        grp.close()
+    (h1, w1, s1), (h0, w0, s0) = out
+    for it in range(iters):
+        for k in ("states", "log_probs", "values"):
+            assert torch.equal(h1[it][k], h0[it][k]), (it, k)
+        assert h1[it]["metrics"] == h0[it]["metrics"], it
+    assert all(torch.equal(a, b) for a, b in zip(w1, w0))
+    assert s1["rollout_capture"] >= 1 and s0.get("rollout_capture", 0) == 0
