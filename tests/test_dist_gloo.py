@@ -1,9 +1,10 @@
-"""Env-sharded data parallelism on CPU with gloo, world size 2.
+"""Env-sharded data parallelism on CPU with gloo, world sizes 2 and 4.
 
 Each rank owns its own slice of samples; per optimizer step the flat gradient bucket is
 all-reduced (mean), and advantage statistics are reduced once per update.  The sharded result
 must equal one process running the same update on the concatenated data with global
-minibatch i = rank0's minibatch i ++ rank1's minibatch i."""
+minibatch i = rank0's minibatch i ++ rank1's minibatch i ++ ... (world 4 rehearses more ranks
+than the one-GPU box can run)."""
 
 import os
 import socket
@@ -55,8 +56,8 @@ def _worker(rank, world, port, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(1)
-    if rank == 1:
-        torch.manual_seed(999)  # different local init: the broadcast must make weights equal
+    if rank > 0:
+        torch.manual_seed(999 + rank)  # different local init: the broadcast must make weights equal
     agent = _make_agent(torch.distributed.group.WORLD)
     d = _data(rank)
     adv_n = agent.normalize_advantages(d["a"])
@@ -68,28 +69,29 @@ def _worker(rank, world, port, out_dir):
     torch.distributed.destroy_process_group()
 
 
-def test_sharded_update_equals_single_process(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_update_equals_single_process(tmp_path, world):
     port = _free_port()
-    mp.start_processes(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True,
+    mp.start_processes(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
-    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
-    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    rs = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
     # replicas stay identical
-    for k in r0["state"]:
-        torch.testing.assert_close(r0["state"][k], r1["state"][k], rtol=0, atol=0)
+    for r in rs[1:]:
+        for k in rs[0]["state"]:
+            torch.testing.assert_close(rs[0]["state"][k], r["state"][k], rtol=0, atol=0)
     # single process on the concatenated data
-    d0, d1 = _data(0), _data(1)
-    cat = {k: torch.cat([d0[k], d1[k]]) for k in ("s", "z", "lp", "a", "r")}
+    ds = [_data(r) for r in range(world)]
+    cat = {k: torch.cat([d[k] for d in ds]) for k in ("s", "z", "lp", "a", "r")}
     a = cat["a"]
     adv_n = (a - a.mean()) / (a.std() + 1e-8)
-    torch.testing.assert_close(torch.cat([r0["adv"], r1["adv"]]), adv_n, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(torch.cat([r["adv"] for r in rs]), adv_n, rtol=1e-5, atol=1e-6)
     agent = _make_agent(None)
     mb = NLOC // NMB
-    batches = [torch.cat([d0["perm"][i * mb:(i + 1) * mb], d1["perm"][i * mb:(i + 1) * mb] + NLOC])
+    batches = [torch.cat([d["perm"][i * mb:(i + 1) * mb] + r * NLOC for r, d in enumerate(ds)])
                for i in range(NMB)]
     agent._run_epochs(cat["s"], cat["z"], cat["lp"], adv_n, cat["r"], batches)
     for k, v in agent.actor_critic.state_dict().items():
-        torch.testing.assert_close(r0["state"][k], v, rtol=2e-5, atol=2e-6, msg=k)
+        torch.testing.assert_close(rs[0]["state"][k], v, rtol=2e-5, atol=2e-6, msg=k)
 
 
 # ---- the runner's episode stream over ranks (training/routine.py _episode_ends) ----
