@@ -46,8 +46,8 @@ def _worker(rank, world, port, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", 0)
-    if rank == 1:
-        torch.manual_seed(999)  # different local init: the broadcast must make weights equal
+    if rank > 0:
+        torch.manual_seed(999 + rank)  # different local init: the broadcast must make weights equal
     from hwy.ppo_native import FusedPPO
 
     agent = _agent(dev, torch.distributed.group.WORLD)
@@ -61,26 +61,30 @@ def _worker(rank, world, port, out_dir):
     torch.distributed.destroy_process_group()
 
 
-def test_fused_sharded_update_equals_single_process(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_fused_sharded_update_equals_single_process(tmp_path, world):
+    """world 4: four gloo ranks on the one GPU, rehearsing more ranks than the box has cards."""
     port = _free_port()
-    mp.start_processes(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True,
+    mp.start_processes(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
-    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
-    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
-    for k in r0["state"]:  # replicas stay identical
-        torch.testing.assert_close(r0["state"][k], r1["state"][k], rtol=0, atol=0)
+    rs = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
+    r0 = rs[0]
+    for r in rs[1:]:  # replicas stay identical
+        for k in r0["state"]:
+            torch.testing.assert_close(r0["state"][k], r["state"][k], rtol=0, atol=0)
     from hwy.ppo_native import FusedPPO
 
     dev = torch.device("cuda", 0)
-    d0, d1 = _data(0, dev), _data(1, dev)
-    cat = {k: torch.cat([d0[k], d1[k]]) for k in ("s", "z", "lp", "a", "r")}
+    ds = [_data(r, dev) for r in range(world)]
+    cat = {k: torch.cat([d[k] for d in ds]) for k in ("s", "z", "lp", "a", "r")}
     adv = (cat["a"] - cat["a"].mean()) / (cat["a"].std() + 1e-8)
-    torch.testing.assert_close(torch.cat([r0["adv"], r1["adv"]]).to(dev), adv, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(torch.cat([r["adv"] for r in rs]).to(dev), adv, rtol=1e-5,
+                               atol=1e-6)
     mb = NLOC // NMB
-    perm = torch.cat([torch.cat([d0["perm"][i * mb:(i + 1) * mb], d1["perm"][i * mb:(i + 1) * mb] + NLOC])
-                      for i in range(NMB)])
+    perm = torch.cat([torch.cat([d["perm"][i * mb:(i + 1) * mb] + r * NLOC
+                                 for r, d in enumerate(ds)]) for i in range(NMB)])
     agent = _agent(dev)
-    F = FusedPPO(agent, 2 * mb, NMB, use_graphs=True)
+    F = FusedPPO(agent, world * mb, NMB, use_graphs=True)
     F.run(cat["s"], cat["z"].contiguous(), cat["lp"], adv.contiguous(), cat["r"], perm.contiguous())
     torch.cuda.synchronize()
     steps = EPOCHS * NMB
