@@ -254,6 +254,66 @@ int hwy_step(hwy_handle* h, const float* actions, float* obs, float* reward, uin
   return HWY_OK;
 }
 
+int64_t hwy_step_group_table_bytes(int n) {
+  return n < 1 ? -1 : (int64_t)n * (int64_t)sizeof(StepParams);
+}
+
+int hwy_step_group_prepare(hwy_handle* const* handles, const hwy_step_io* io, int n, void* table,
+                           hwy_step_group_plan* plan, void* stream) {
+  if (!handles || !io || n < 1 || !table || !plan)
+    return fail(HWY_EINVAL, "hwy_step_group_prepare: handles/io/table/plan NULL or n < 1");
+  StepParams* tab = new StepParams[n];
+  int blocks = 0, dev = -1;
+  int64_t total = 0;
+  for (int i = 0; i < n; ++i) {
+    hwy_handle* h = handles[i];
+    const hwy_step_io& a = io[i];
+    if (!h || !a.actions || !a.obs || !a.reward || !a.terminated || !a.truncated) {
+      delete[] tab;
+      return fail(HWY_EINVAL, "hwy_step_group_prepare: handle %d or its actions/obs/reward/"
+                              "terminated/truncated is NULL", i);
+    }
+    if (dev >= 0 && h->device != dev) {
+      delete[] tab;
+      return fail(HWY_EINVAL, "hwy_step_group_prepare: handles on devices %d and %d", dev,
+                  h->device);
+    }
+    dev = h->device;
+    StepParams p = params_of(h);
+    p.actions = a.actions;
+    p.obs = a.obs;
+    p.reward = a.reward;
+    p.term = a.terminated;
+    p.trunc = a.truncated;
+    p.ep_ret = a.ep_return;
+    p.ep_len = a.ep_length;
+    tab[i] = p;
+    const int b = hwy_step_blocks(h->cfg.num_envs);
+    blocks = b > blocks ? b : blocks;
+    total += h->cfg.num_envs;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipStreamSynchronize(s);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(table, tab, (size_t)n * sizeof(StepParams), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  delete[] tab;
+  if (e != hipSuccess) return hip_fail(e, "hwy_step_group_prepare");
+  plan->n = n;
+  plan->blocks = blocks;
+  plan->big = hwy_step_big(total);
+  return HWY_OK;
+}
+
+int hwy_step_group(const hwy_step_group_plan* plan, const void* table, void* stream) {
+  if (!plan || !table || plan->n < 1 || plan->blocks < 1)
+    return fail(HWY_EINVAL, "hwy_step_group: empty plan or NULL table");
+  if (hwy_launch_step_group((const StepParams*)table, plan->n, plan->blocks, plan->big,
+                            (hipStream_t)stream))
+    return hip_fail(hipGetLastError(), "hwy_step_grp_kernel");
+  return HWY_OK;
+}
+
 int hwy_export_state(hwy_handle* h, uint32_t* dst, void* stream) {
   if (!h || !dst) return fail(HWY_EINVAL, "handle/dst is NULL");
   size_t bytes = (size_t)HWY_NFIELDS * h->cfg.num_envs * HWY_MAX_VEHICLES * sizeof(uint32_t);

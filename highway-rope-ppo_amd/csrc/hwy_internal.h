@@ -29,6 +29,11 @@ struct StepParams {
 
 extern "C" {
 int hwy_launch_step(const StepParams* p, hipStream_t s);
+// n handles' steps in one launch: dtab = n StepParams in device memory, blocks = the largest
+// handle's hwy_step_blocks, big = hwy_step_big(total envs) (the register budget of the launch)
+int hwy_launch_step_group(const StepParams* dtab, int n, int blocks, int big, hipStream_t s);
+int hwy_step_blocks(int num_envs);
+int hwy_step_big(int64_t total_envs);
 int hwy_launch_reset(const StepParams* p, hipStream_t s);
 int hwy_launch_obs_pe(const float* in, float* out, int E, int N, int F, int kind, int d, int ego,
                       float max_dist, const float* table, const float* dov, hipStream_t s);

@@ -1233,9 +1233,11 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
 // outside the hot loop) when more envs queue behind them: 16,384 envs 0.412 -> 0.365 ms,
 // 32,768 0.775 -> 0.670 (5 waves: 0.381 / 0.702), 8,192 0.228 -> 0.220; at 4,096 envs the 6-wave
 // build takes 0.164 ms, so hwy_launch_step picks by env count
+// The step of one handle's envs; the kernels below run it for one handle (hwy_step) or for
+// handle blockIdx.y of a table (hwy_step_group: a sweep's cells in one launch).  It reads no
+// gridDim and no blockIdx.y, so a grouped launch computes every env exactly as its handle's own.
 template <int W>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8)))
-hwy_step_kernel(StepParams P) {
+__device__ __forceinline__ void step_body(const StepParams& P) {
   __shared__ int lds_vor[ENVS_PER_BLOCK][WAVE];
   __shared__ int lds_inv[ENVS_PER_BLOCK][WAVE];
   __shared__ CollLds lds_coll[ENVS_PER_BLOCK];
@@ -1365,6 +1367,20 @@ hwy_step_kernel(StepParams P) {
   WAVE_T(e, lane, 4, __builtin_amdgcn_s_memrealtime());
   WAVE_T(e, lane, 2, (unsigned long long)done | WAVE_HWID());
   SEC_FLUSH(sp, lane, e);
+}
+
+template <int W>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8)))
+hwy_step_kernel(StepParams P) {
+  step_body<W>(P);
+}
+
+// handle blockIdx.y of tab; blocks past a handle's envs exit in step_body (whole waves).  The
+// profiling builds' per-env clocks and section counters index by env within the handle.
+template <int W>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8)))
+hwy_step_grp_kernel(const StepParams* __restrict__ tab) {
+  step_body<W>(tab[blockIdx.y]);
 }
 
 __global__ void __launch_bounds__(256) hwy_reset_kernel(StepParams P) {
@@ -1513,6 +1529,17 @@ int hwy_launch_step(const StepParams* p, hipStream_t s) {
     hipLaunchKernelGGL(hwy_step_kernel<4>, dim3(blocks), dim3(ENVS_PER_BLOCK * WAVE), 0, s, *p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+int hwy_launch_step_group(const StepParams* dtab, int n, int blocks, int big, hipStream_t s) {
+  if (big)
+    hipLaunchKernelGGL(hwy_step_grp_kernel<kStepBigW>, dim3(blocks, n), dim3(ENVS_PER_BLOCK * WAVE),
+                       0, s, dtab);
+  else
+    hipLaunchKernelGGL(hwy_step_grp_kernel<4>, dim3(blocks, n), dim3(ENVS_PER_BLOCK * WAVE), 0, s,
+                       dtab);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int hwy_step_blocks(int num_envs) { return (num_envs + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK; }
+int hwy_step_big(int64_t total_envs) { return total_envs > (int64_t)16 * device_cus() ? 1 : 0; }
 int hwy_launch_reset(const StepParams* p, hipStream_t s) {
   const int blocks = (p->cfg.num_envs + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
   hipLaunchKernelGGL(hwy_reset_kernel, dim3(blocks), dim3(ENVS_PER_BLOCK * WAVE), 0, s, *p);

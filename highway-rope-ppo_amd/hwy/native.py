@@ -29,6 +29,16 @@ class HwyNativeError(RuntimeError):
 _lib = None
 
 
+class HwyStepIO(ctypes.Structure):
+    """hwy_step_io (include/hwy.h): one handle's buffers for a grouped step."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("actions", "obs", "reward", "terminated",
+                                               "truncated", "ep_return", "ep_length")]
+
+
+class HwyStepGroupPlan(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("blocks", ctypes.c_int32), ("big", ctypes.c_int32)]
+
+
 def build(jobs: int = 4) -> str:
     """Compile libhwy.so for gfx950 (hipcc cross-compiles without a GPU)."""
     subprocess.run(["make", "-s", f"-j{jobs}", "-C", CSRC], check=True)
@@ -69,8 +79,13 @@ def lib():
     L.hwy_gae.argtypes = [vp, vp, vp, vp, f64, f64, i32, i32, vp, vp, vp]
     L.hwy_math_selftest.argtypes = [i32, vp, vp, vp, i32, vp]
     L.hwy_set_seed_groups.argtypes = [vp, vp, i32, i32]
+    L.hwy_step_group_table_bytes.argtypes = [i32]
+    L.hwy_step_group_table_bytes.restype = ctypes.c_int64
+    L.hwy_step_group_prepare.argtypes = [vp, vp, i32, vp, ctypes.POINTER(HwyStepGroupPlan), vp]
+    L.hwy_step_group.argtypes = [ctypes.POINTER(HwyStepGroupPlan), vp, vp]
     for name in ("hwy_create", "hwy_obs_features", "hwy_set_pe_table", "hwy_set_seed_schedule",
-                 "hwy_set_seed_groups", "hwy_reset", "hwy_step",
+                 "hwy_set_seed_groups", "hwy_reset", "hwy_step", "hwy_step_group_prepare",
+                 "hwy_step_group",
                  "hwy_export_state", "hwy_import_state", "hwy_obs_pe", "hwy_gae",
                  "hwy_math_selftest"):
         getattr(L, name).restype = i32

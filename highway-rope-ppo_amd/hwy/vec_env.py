@@ -25,7 +25,8 @@ import torch
 from . import _abi
 from ._abi import HWY_MAX_VEHICLES, NFIELDS, PE_NONE, config_from_dict
 from .gym import spaces
-from .native import HwyNativeError, check, lib, ptr, stream_ptr
+from .native import (HwyNativeError, HwyStepGroupPlan, HwyStepIO, check, lib, ptr,
+                     stream_ptr)
 
 
 class HighwayVecEnv:
@@ -252,3 +253,41 @@ class HighwayVecEnv:
     @property
     def unwrapped(self):
         return self
+
+
+class GroupEnvStep:
+    """HighwayVecEnv.step_into for several handles in ONE launch (hwy_step_group): the cells of a
+    sweep batch (ppo/group.py GroupBatch), whose handles differ in observation width and fused
+    wrapper.  Each env computes exactly what its own handle's step computes.  The launch
+    parameters live in a device table per (handle configurations, buffers) key, prepared on first
+    use -- outside any graph capture, as GroupBatch's eager first rollout at a key does -- so the
+    launch itself is graph-capturable."""
+
+    def __init__(self, envs):
+        self.envs = [e.unwrapped if hasattr(e, "unwrapped") else e for e in envs]
+        self.n = len(self.envs)
+        if self.n < 1:
+            raise ValueError("GroupEnvStep needs at least one env")
+        self._nb = int(lib().hwy_step_group_table_bytes(self.n))
+        self._tables: Dict[Any, Any] = {}
+
+    def launch(self, ios) -> None:
+        """ios[i] = (actions, obs, reward, terminated, truncated, ep_return, ep_length) of env i,
+        as step_into takes them (the last two may be None)."""
+        ptrs = tuple(tuple(ptr(x) for x in io) for io in ios)
+        key = (tuple((e._handle.value, e.launch_version) for e in self.envs), ptrs)
+        hit = self._tables.get(key)
+        if hit is None:
+            arr = (HwyStepIO * self.n)()
+            for i, p in enumerate(ptrs):
+                arr[i] = HwyStepIO(*p)
+            hs = (ctypes.c_void_p * self.n)(*[e._handle.value for e in self.envs])
+            dev = self.envs[0].device
+            t = torch.empty(self._nb, dtype=torch.uint8, device=dev)
+            plan = HwyStepGroupPlan()
+            check(lib().hwy_step_group_prepare(hs, arr, self.n, t.data_ptr(), ctypes.byref(plan),
+                                               stream_ptr()), "hwy_step_group_prepare")
+            hit = (t, plan)
+            self._tables[key] = hit
+        check(lib().hwy_step_group(ctypes.byref(hit[1]), hit[0].data_ptr(), stream_ptr()),
+              "hwy_step_group")

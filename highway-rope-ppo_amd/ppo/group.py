@@ -99,12 +99,16 @@ class ExperimentGroup:
         return self.act.rows_of(buf.states[t], (buf.actions[t], buf.pre_tanh[t], buf.log_probs[t],
                                                 buf.values[t]), buf.noise[t])
 
-    def env_step(self, t: int) -> None:
+    def env_io(self, t: int):
+        """step_into's buffers for rollout step t (hwy_step's arguments)."""
         buf, env = self.buf, self.env
         obs_shape = env.obs_buf.shape[1:]
-        env.step_into(buf.actions[t], buf.states[t + 1].view(self.G * self.E, *obs_shape),
-                      buf.rewards[t], buf.terminated[t], buf.truncated[t], buf.ep_return[t],
-                      buf.ep_length[t])
+        return (buf.actions[t], buf.states[t + 1].view(self.G * self.E, *obs_shape),
+                buf.rewards[t], buf.terminated[t], buf.truncated[t], buf.ep_return[t],
+                buf.ep_length[t])
+
+    def env_step(self, t: int) -> None:
+        self.env.step_into(*self.env_io(t))
 
     def _steps(self, tiles) -> None:
         for t in range(self.T):
@@ -304,8 +308,8 @@ class GroupBatch:
     """Several ExperimentGroups of one hidden width and the same rows per learner (a sweep's
     cells that differ only in observation layout, e.g. the four h256 cells: no PE, RoPE, DistPE,
     RankPE, whose state dims are 60 or 120) stepped as ONE set of launches: per rollout step one
-    acting launch for every learner of every group and each group's env step; per minibatch step
-    one grouped fused step over all their learners (hwy_ppo_group_step takes learners of
+    acting launch for every learner of every group and one env launch for every group's handle
+    (hwy_step_group); per minibatch step one grouped fused step over all their learners (hwy_ppo_group_step takes learners of
     different state dims).  Each experiment stays bit-identical to its solo run: the same
     kernel bodies per learner, each group's own generator order, GAE and normalisation."""
 
@@ -318,6 +322,12 @@ class GroupBatch:
             raise ValueError("a batch's groups share envs per experiment and rollout length")
         self.agents = [a for g in self.groups for a in g.agents]
         self.act = GroupAct(self.agents, g0.E)
+        # the groups' env steps as one launch (hwy_step_group): each group's handle alone holds
+        # G x E envs -- one wave each, a small part of the GPU -- so n launches in a row would
+        # leave most of it idle
+        from hwy.vec_env import GroupEnvStep
+
+        self.envstep = GroupEnvStep([g.env for g in self.groups]) if len(self.groups) > 1 else None
         self.use_graphs = bool(use_graphs)
         self.T = g0.T
         self._roll = (None, None, None)
@@ -331,8 +341,10 @@ class GroupBatch:
     def _steps(self, tiles):
         for t in range(self.T):
             self.act.launch(self._rows(t), tiles)
-            for g in self.groups:
-                g.env_step(t)
+            if self.envstep is not None:
+                self.envstep.launch([g.env_io(t) for g in self.groups])
+            else:
+                self.groups[0].env_step(t)
         for g in self.groups:
             g.buf.finish_dones()
 

@@ -23,6 +23,7 @@
  *                                RankEmbedWrapper.observation            experiments/rank_embed.py:45-51
  *   hwy_gae                   <- PPOMemory.compute_advantages            ppo/agent.py:126-138
  *   hwy_set_seed_groups       <- one gym.make per experiment of a sweep  experiments/runner.py:73-78
+ *   hwy_step_group            <- env.step of every cell of a sweep batch (one launch)
  *                                (main.py:188-242 fans the seeds out as separate processes; here
  *                                 a cell's seeds share one handle, each with its own schedule)
  *
@@ -197,6 +198,32 @@ int hwy_reset(hwy_handle* h, const uint64_t* seeds, const uint8_t* mask, float* 
  *   holds the first observation of the next episode. */
 int hwy_step(hwy_handle* h, const float* actions, float* obs, float* reward, uint8_t* terminated,
              uint8_t* truncated, float* ep_return, int32_t* ep_length, void* stream);
+
+/* ---- Grouped step: n handles (the cells of a sweep batch, each one experiment group's handle;
+ * ppo/group.py GroupBatch) stepped in ONE launch instead of n.  Workgroup (x, y) runs hwy_step's
+ * workgroup x for handle y, reading that handle's launch parameters from a device table; each
+ * env computes exactly what hwy_step on its own handle computes (the same kernel body).  Handles
+ * may differ in env count, observation width and fused wrapper; one launch takes the register
+ * budget of the handles' total env count.  hwy_step_group_prepare builds the table from the
+ * handles as they are now and the per-handle buffers io[i] (hwy_step's arguments); it is
+ * synchronous (waits for `stream`) and must be redone after any handle's configuration changes
+ * (seed schedule, groups, PE table).  hwy_step_group is asynchronous and hipGraph-capturable. */
+typedef struct hwy_step_io {
+  const float* actions;
+  float* obs;
+  float* reward;
+  uint8_t* terminated;
+  uint8_t* truncated;
+  float* ep_return;  /* nullable */
+  int32_t* ep_length; /* nullable */
+} hwy_step_io;
+typedef struct hwy_step_group_plan {
+  int32_t n, blocks, big; /* handles; workgroups per handle (the largest); register budget */
+} hwy_step_group_plan;
+int64_t hwy_step_group_table_bytes(int n);
+int hwy_step_group_prepare(hwy_handle* const* handles, const hwy_step_io* io, int n, void* table,
+                           hwy_step_group_plan* plan, void* stream);
+int hwy_step_group(const hwy_step_group_plan* plan, const void* table, void* stream);
 
 /* Copy the packed state [HWY_NFIELDS][E][HWY_MAX_VEHICLES] u32 to / from device memory. */
 int hwy_export_state(hwy_handle* h, uint32_t* dst, void* stream);

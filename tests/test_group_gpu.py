@@ -217,3 +217,66 @@ def test_group_eager_equals_graph_replay():
         assert h1[it]["metrics"] == h0[it]["metrics"], it
     assert all(torch.equal(a, b) for a, b in zip(w1, w0))
     assert s1["rollout_capture"] >= 1 and s0.get("rollout_capture", 0) == 0
+
+
+def test_grouped_env_step_equals_each_handles_own_step():
+    """hwy_step_group: three handles that differ in env count, observation width, row order and
+    fused wrapper (sorted / no PE, 8 envs; shuffled RoPE, 16; RankPE with seed groups, 3 x 8)
+    stepped as ONE launch produce, step for step, exactly what each handle's own hwy_step
+    produces: observations, rewards, flags and finished-episode returns and lengths, through
+    crashes and in-kernel autoresets."""
+    from config.base_config import HIGHWAY_CONFIG
+    from experiments.config import Condition
+    from experiments.wrappers import make_env
+    from hwy.vec_env import GroupEnvStep
+    from utils.reproducibility import set_random_seeds
+
+    specs = [(Condition.SORTED, None, 8, {}, None),
+             (Condition.SHUFFLED_ROPE, 4, 16, {"observation": {"order": "shuffled"}}, None),
+             (Condition.SHUFFLED_RANKPE, 4, 24, {}, [5, 900, 77])]
+
+    def make_set():
+        envs = []
+        for i, (cond, d, E, ov, groups) in enumerate(specs):
+            set_random_seeds(1000 + i)  # RankPE draws its table from the global RNG
+            env = make_env(cond, HIGHWAY_CONFIG, d_embed=d,
+                           env_overrides=dict(ov, num_envs=E, device=DEV, autoreset=True))
+            if hasattr(env, "to"):
+                env = env.to(DEV)
+            base = env.unwrapped
+            if groups:
+                base.set_seed_groups(groups, E // len(groups))
+            else:
+                base.set_seed_schedule(31 + i)
+            env.reset()
+            envs.append(base)
+        return envs
+
+    solo, grouped = make_set(), make_set()
+    gstep = GroupEnvStep(grouped)
+
+    def bufs(env):
+        E = env.num_envs
+        return (torch.empty(E, 2, device=DEV), torch.empty_like(env.obs_buf),
+                torch.empty(E, device=DEV), torch.empty(E, dtype=torch.uint8, device=DEV),
+                torch.empty(E, dtype=torch.uint8, device=DEV), torch.empty(E, device=DEV),
+                torch.empty(E, dtype=torch.int32, device=DEV))
+
+    bs, bg = [bufs(e) for e in solo], [bufs(e) for e in grouped]
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    episodes = 0
+    for step in range(60):
+        for a, b in zip(bs, bg):
+            a[0].copy_(torch.rand(a[0].shape, device=DEV, generator=gen) * 2 - 1)
+            b[0].copy_(a[0])
+        for env, a in zip(solo, bs):
+            env.step_into(*a)
+        gstep.launch(bg)
+        torch.cuda.synchronize()
+        for i, (a, b) in enumerate(zip(bs, bg)):
+            for k in range(1, 7):
+                assert torch.equal(a[k], b[k]), (step, i, k)
+            episodes += int((a[3] | a[4]).sum())
+    assert episodes > 0  # autoresets happened inside the compared window
+    for env in solo + grouped:
+        env.close()
