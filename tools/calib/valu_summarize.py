@@ -7,13 +7,15 @@ root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmck"
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 15
 Fo = int(sys.argv[3]) if len(sys.argv) > 3 else 4
 agg = collections.defaultdict(list)
+names = set()
 for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         if "hwy_step" in r["Kernel_Name"]:
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            names.add(r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0].strip())
 m = {k: sum(v) / len(v) for k, v in agg.items()}
 E = int(round(m["SQ_WAVES"]))
-res = {"kernel": "hwy_step_kernel", "envs_per_launch": E, "obs_rows": N, "obs_features": Fo,
+res = {"kernel": " + ".join(sorted(names)), "envs_per_launch": E, "obs_rows": N, "obs_features": Fo,
        "valu_insts_per_launch": m["SQ_INSTS_VALU"], "salu_insts_per_launch": m["SQ_INSTS_SALU"],
        "lds_insts_per_launch": m["SQ_INSTS_LDS"], "branch_insts_per_launch": m["SQ_INSTS_BRANCH"],
        "waves_per_launch": m["SQ_WAVES"], "valu_insts_per_wave": m["SQ_INSTS_VALU"] / m["SQ_WAVES"],
