@@ -165,3 +165,30 @@ def test_group_table_geometry_without_gpu(lib):
     g = lib.hwy_ppo_group_act_table_bytes
     g.restype = ctypes.c_int64
     assert g(10) > g(1) > 0 and g(0) == -1
+
+
+def test_step_group_table_and_argument_checks_without_gpu(lib):
+    """hwy_step_group (include/hwy.h): the table holds one launch-parameter record per handle,
+    and a prepare or launch with missing arguments is refused before any device call."""
+    from hwy.native import HwyStepGroupPlan, HwyStepIO
+
+    f = lib.hwy_step_group_table_bytes
+    f.restype = ctypes.c_int64
+    f.argtypes = [ctypes.c_int]
+    one = f(1)
+    assert one > 0 and f(4) == 4 * one and f(0) == -1
+    p = lib.hwy_step_group_prepare
+    p.restype = ctypes.c_int
+    p.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                  ctypes.POINTER(HwyStepGroupPlan), ctypes.c_void_p]
+    plan = HwyStepGroupPlan()
+    io = (HwyStepIO * 1)()
+    assert p(None, io, 1, None, ctypes.byref(plan), None) == -1
+    handles = (ctypes.c_void_p * 1)(None)
+    assert p(handles, io, 1, ctypes.c_void_p(16), ctypes.byref(plan), None) == -1  # NULL handle
+    lib.hwy_last_error.restype = ctypes.c_char_p
+    assert b"NULL" in lib.hwy_last_error()
+    s = lib.hwy_step_group
+    s.restype = ctypes.c_int
+    s.argtypes = [ctypes.POINTER(HwyStepGroupPlan), ctypes.c_void_p, ctypes.c_void_p]
+    assert s(ctypes.byref(HwyStepGroupPlan(0, 0, 0)), ctypes.c_void_p(16), None) == -1
