@@ -174,57 +174,85 @@ class ExperimentRunner:
         (main.py:188-242, utils/device_pool.py:44-72).  Needs the vectorised loop
         (extra["num_envs"] > 1) and the fused HIP learner; returns one status dict per experiment,
         in order."""
+        return self.launch_batch([exps])[0]
+
+    def launch_batch(self, cells) -> list:
+        """launch_group for several cells at once: each cell (experiments that differ only in
+        seed) becomes an ExperimentGroup, and the cells, which must share envs per experiment,
+        rollout length and hidden width (e.g. a sweep's four h256 conditions, whose state dims
+        differ), are stepped together by one GroupBatch: one acting launch, one env launch and
+        one grouped minibatch step for all their learners.  Every experiment stays bit-identical
+        to its solo launch().  Returns one list of status dicts per cell."""
         import math
 
-        from ppo.group import build_group
-        from training.routine import train_group
+        from ppo.group import GroupBatch, build_group
+        from training.routine import train_batch
 
-        exps = list(exps)
+        cells = [list(c) for c in cells]
         t0 = time.time()
-        key = {(e.condition, repr(e.hp), repr(sorted(e.extra.items())),
-                repr(e.env_config_overrides), e.max_episodes, e.target_reward) for e in exps}
-        if len(key) != 1:
-            raise ValueError("launch_group: the experiments must differ only in seed and name")
-        e0 = exps[0]
-        E = int(e0.extra.get("num_envs", 1))
-        if E <= 1:
-            raise ValueError("launch_group needs extra['num_envs'] > 1 (the vectorised loop)")
-        results = [{"experiment_name": e.name, "status": "FAILED"} for e in exps]
+        for exps in cells:
+            key = {(e.condition, repr(e.hp), repr(sorted(e.extra.items())),
+                    repr(e.env_config_overrides), e.max_episodes, e.target_reward) for e in exps}
+            if len(key) != 1:
+                raise ValueError("launch_group: the experiments must differ only in seed and name")
+            if int(exps[0].extra.get("num_envs", 1)) <= 1:
+                raise ValueError("launch_group needs extra['num_envs'] > 1 (the vectorised loop)")
+        first = [c[0] for c in cells]
+        shared = {(int(e.extra.get("num_envs", 1)), e.hp.steps_per_update, e.hp.hidden_dim,
+                   e.max_episodes, e.target_reward, e.extra.get("eval_interval", 50))
+                  for e in first}
+        if len(shared) != 1:
+            raise ValueError("launch_batch: the cells must share num_envs, steps_per_update, "
+                             "hidden_dim, max_episodes, target_reward and eval_interval")
+        results = [[{"experiment_name": e.name, "status": "FAILED"} for e in exps]
+                   for exps in cells]
         loggers = []
-        grp = None
+        groups = []
         try:
             with self.pool.acquire() as device:
-                for e in exps:
-                    set_random_seeds(e.seed)  # as launch() does before the logger
-                    lg = setup_experiment_logger(e.name)
-                    lg.info(f"[{e.name}] Acquired device: {device} | Seed: {e.seed} | group of "
-                            f"{len(exps)}")
-                    loggers.append(lg)
-                T = max(1, math.ceil(e0.hp.steps_per_update / E))
-                lg_iter = iter(loggers)
+                for exps in cells:
+                    e0 = exps[0]
+                    E = int(e0.extra.get("num_envs", 1))
+                    cell_loggers = []
+                    for e in exps:
+                        set_random_seeds(e.seed)  # as launch() does before the logger
+                        lg = setup_experiment_logger(e.name)
+                        lg.info(f"[{e.name}] Acquired device: {device} | Seed: {e.seed} | group "
+                                f"of {len(exps)}")
+                        cell_loggers.append(lg)
+                    loggers += cell_loggers
+                    T = max(1, math.ceil(e0.hp.steps_per_update / E))
+                    lg_iter = iter(cell_loggers)
 
-                def make_agent(sd):
-                    return self._create_agent(sd, 2, e0.hp, next(lg_iter), device, e0.extra)
+                    def make_agent(sd, e0=e0, lg_iter=lg_iter):
+                        return self._create_agent(sd, 2, e0.hp, next(lg_iter), device, e0.extra)
 
-                grp = build_group(e0.condition, self.base_config, [e.seed for e in exps], E, T,
-                                  device, make_agent, d_embed=e0.hp.d_embed,
-                                  env_overrides=e0.env_config_overrides)
-                outs = train_group(grp, [e.name for e in exps], [e.seed for e in exps],
+                    groups.append(build_group(e0.condition, self.base_config,
+                                              [e.seed for e in exps], E, T, device, make_agent,
+                                              d_embed=e0.hp.d_embed,
+                                              env_overrides=e0.env_config_overrides))
+                stepper = groups[0] if len(groups) == 1 else GroupBatch(groups)
+                e0 = first[0]
+                outs = train_batch(stepper, groups, [e.name for c in cells for e in c],
+                                   [e.seed for c in cells for e in c],
                                    max_episodes=e0.max_episodes, target_reward=e0.target_reward,
                                    log_interval=e0.extra.get("log_interval", 20),
                                    eval_interval=e0.extra.get("eval_interval", 50),
                                    loggers=loggers)
-                for res, (rewards, avg_rewards, metrics) in zip(results, outs):
+                flat = [res for cell in results for res in cell]
+                for res, (rewards, avg_rewards, metrics) in zip(flat, outs):
                     res.update(status="COMPLETED", rewards=rewards, avg_rewards=avg_rewards,
                                metrics_history=metrics)
         except Exception as ex:
-            for res in results:
-                res["error_message"] = str(ex)
-                res["error_traceback"] = traceback.format_exc()
+            for cell in results:
+                for res in cell:
+                    res["error_message"] = str(ex)
+                    res["error_traceback"] = traceback.format_exc()
         finally:
-            if grp is not None:
-                grp.close()
-        for res in results:
-            res["duration_seconds"] = time.time() - t0
+            for g in groups:
+                g.close()
+        for cell in results:
+            for res in cell:
+                res["duration_seconds"] = time.time() - t0
         logging.shutdown()
         return results

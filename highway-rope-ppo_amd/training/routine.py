@@ -365,38 +365,58 @@ def train_group(group, experiment_names, exp_seeds, max_episodes=500, target_rew
     Returns, per experiment, the reference's (rewards, avg_rewards, metrics_history), each equal
     to its solo run's: the group's experiments are bit-identical to solo runs
     (tests/test_group_gpu.py) and evaluation draws no random numbers."""
-    G, E, T = group.G, group.E, group.T
+    return train_batch(group, [group], experiment_names, exp_seeds, max_episodes=max_episodes,
+                       target_reward=target_reward, log_interval=log_interval,
+                       eval_interval=eval_interval, loggers=loggers)
+
+
+def train_batch(stepper, groups, experiment_names, exp_seeds, max_episodes=500, target_reward=0.0,
+                log_interval=20, eval_interval=50, loggers=None):
+    """train_group over the experiments of several ExperimentGroups stepped together: `stepper`
+    is the ExperimentGroup itself (groups = [it]) or a GroupBatch over `groups` (ppo/group.py:
+    the cells of one hidden width in one set of launches).  experiment_names / exp_seeds /
+    loggers list every group's experiments in group order; each experiment's bookkeeping is its
+    solo run's, on its own [T, E] slice of its group's rollout."""
+    members = [(g, j) for g in groups for j in range(g.G)]
+    if len(experiment_names) != len(members) or len(exp_seeds) != len(members):
+        raise ValueError(f"train_batch: {len(members)} experiments, "
+                         f"{len(experiment_names)} names, {len(exp_seeds)} seeds")
     artifacts_dir = ensure_artifacts_dir()
     checkpoint_dir = os.path.join(artifacts_dir, "checkpoints")
     os.makedirs(checkpoint_dir, exist_ok=True)
     start_time = time.time()
     runs = []
-    for g in range(G):
-        name = experiment_names[g]
-        logger = loggers[g] if loggers else setup_experiment_logger(name)
+    for k, (grp, j) in enumerate(members):
+        name = experiment_names[k]
+        logger = loggers[k] if loggers else setup_experiment_logger(name)
         prefix = f"[{name}]" if name else ""
-        logger.info(f"{prefix} Starting training for experiment: {name} (group of {G})")
+        logger.info(f"{prefix} Starting training for experiment: {name} (group of {grp.G}, "
+                    f"batch of {len(members)})")
         mh = {"experiment_name": name, "episode_rewards": [], "eval_rewards": [],
               "avg_eval_rewards": [], "policy_updates": [], "episode_numbers": [],
               "eval_episode_numbers": [], "timestamps": []}
-        tracker = _EvalTracker(group.solo_envs[g], group.agents[g], int(exp_seeds[g]),
+        tracker = _EvalTracker(grp.solo_envs[j], grp.agents[j], int(exp_seeds[k]),
                                target_reward, checkpoint_dir, name, mh, logger, prefix, start_time)
         logger.info(f"{prefix} Performing initial evaluation...")
         tracker.initial()
         runs.append({"name": name, "logger": logger, "prefix": prefix, "mh": mh,
                      "tracker": tracker, "episode_rewards": [], "training_episodes": [],
-                     "episode_num": 0, "total_steps": 0, "done": max_episodes <= 0})
-    buf = group.buf
+                     "episode_num": 0, "total_steps": 0, "done": max_episodes <= 0,
+                     "group": grp, "j": j})
     while not all(r["done"] for r in runs):
         t_update = time.time()
-        group.rollout()
-        upds = group.update(return_metrics=True)
-        for g, r in enumerate(runs):
+        stepper.rollout()
+        upds = stepper.update(return_metrics=True)
+        if len(groups) > 1 or stepper is not groups[0]:  # a GroupBatch: one list per group
+            upds = [m for per_group in upds for m in per_group]
+        for r, upd in zip(runs, upds):
             if r["done"]:
                 continue
+            grp, j = r["group"], r["j"]
+            E, T = grp.E, grp.T
             r["total_steps"] += T * E
-            sl = slice(g * E, (g + 1) * E)
-            for ret in _episode_ends(buf.dones[:, sl], buf.ep_return[:, sl]):
+            sl = slice(j * E, (j + 1) * E)
+            for ret in _episode_ends(grp.buf.dones[:, sl], grp.buf.ep_return[:, sl]):
                 if r["episode_num"] >= max_episodes:
                     break
                 r["episode_num"] += 1
@@ -410,7 +430,7 @@ def train_group(group, experiment_names, exp_seeds, max_episodes=500, target_rew
                 if r["episode_num"] % eval_interval == 0:
                     r["tracker"].on_episode(r["episode_num"])
             r["mh"]["policy_updates"].append({"episode": r["episode_num"], "steps": T * E,
-                                              "time": time.time() - t_update, **upds[g]})
+                                              "time": time.time() - t_update, **upd})
             if r["episode_num"] >= max_episodes:
                 r["done"] = True
     out = []

@@ -280,3 +280,38 @@ def test_grouped_env_step_equals_each_handles_own_step():
     assert episodes > 0  # autoresets happened inside the compared window
     for env in solo + grouped:
         env.close()
+
+
+def test_runner_launch_batch_equals_launch_group(tmp_path, monkeypatch):
+    """ExperimentRunner.launch_batch (two h256 cells of different state dims stepped by one
+    GroupBatch, training/routine.py:train_batch) returns, per experiment, exactly what
+    launch_group returns for its cell alone."""
+    from config.base_config import HIGHWAY_CONFIG
+    from experiments.config import Condition, ConditionHP, Experiment
+    from experiments.runner import ExperimentRunner
+
+    monkeypatch.chdir(tmp_path)
+
+    def exp(cond, d, seed):
+        hp = ConditionHP(lr=3e-4, clip_eps=0.2, epochs=2, batch_size=64, hidden_dim=256,
+                         d_embed=d)
+        hp.entropy_coef = 0.005
+        hp.steps_per_update = 16 * 32
+        return Experiment(name=f"b_{cond.name}_{seed}", condition=cond, hp=hp, seed=seed,
+                          max_episodes=24, target_reward=1e9,
+                          extra={"num_envs": 16, "num_minibatches": 8, "eval_interval": 8,
+                                 "log_interval": 50}, env_config_overrides={})
+
+    cells = [[exp(Condition.SORTED, None, s) for s in (42, 1042)],
+             [exp(Condition.SHUFFLED_RANKPE, 4, s) for s in (7, 2042)]]
+    batched = ExperimentRunner(HIGHWAY_CONFIG).launch_batch(cells)
+    for cell, got in zip(cells, batched):
+        alone = ExperimentRunner(HIGHWAY_CONFIG).launch_group(cell)
+        for a, b in zip(alone, got):
+            assert a["status"] == b["status"] == "COMPLETED", (a.get("error_message"),
+                                                               b.get("error_message"))
+            assert a["rewards"] == b["rewards"] and a["avg_rewards"] == b["avg_rewards"]
+            ma, mb = a["metrics_history"], b["metrics_history"]
+            assert ma["episode_rewards"] == mb["episode_rewards"]
+            assert [u["loss"] for u in ma["policy_updates"]] == \
+                [u["loss"] for u in mb["policy_updates"]]

@@ -17,7 +17,7 @@ reproduce them exactly.  Also writes OUT/sweep.json (wall time, per-cell agreeme
 one line per cell.
 
     python tools/sweep_reward.py --out gpurun_out/sweep_reward [--cells sorted_h256 ...]
-        [--seeds 42 1042 ...] [--work /tmp/sweep_work]
+        [--seeds 42 1042 ...] [--work /tmp/sweep_work] [--batch]
 """
 
 from __future__ import annotations
@@ -38,6 +38,60 @@ CELLS = {"sorted_h256": ("sorted", 256), "sorted_h384": ("sorted", 384),
          "shuffled_rankpe_h256": ("shuffled_rankpe", 256)}
 
 
+def _write_cell(out, cell, exps, results, wall, unit_cells, E, T, M, args, reference_final):
+    """summary.jsonl of one cell (tools/condition_order.py layout) and its report entry."""
+    cname, H = CELLS[cell]
+    d_embed = None if cname == "sorted" else 4
+    run_dir = os.path.join(out, f"{cname}_h{H}_e{E}_t{T}")
+    os.makedirs(run_dir, exist_ok=True)
+    solo = {}
+    solo_path = os.path.join(ROOT, "profiles", "r4", "reward", f"{cell}_e{E}_t{T}",
+                             "summary.jsonl")
+    if os.path.exists(solo_path):
+        for line in open(solo_path):
+            r = json.loads(line)
+            if r.get("episodes") == args.episodes and r.get("eval_interval") == args.eval_interval:
+                solo[int(r["seed"])] = r.get("final_reward")
+    rows, same = [], []
+    ref = reference_final(cname, H)
+    with open(os.path.join(run_dir, "summary.jsonl"), "w") as f:
+        for e, res in zip(exps, results):
+            row = {"condition": cname, "seed": e.seed, "experiment": e.name,
+                   "status": res["status"], "num_envs": E, "episodes": args.episodes,
+                   "rollout": T, "minibatches": M, "eval_interval": args.eval_interval,
+                   "lr": 3e-4, "epochs": 8, "hidden_dim": H, "obs_vehicles": 15,
+                   "order": "make_env default", "d_embed": d_embed, "grouped": len(exps),
+                   "cells_in_batch": unit_cells}
+            if res["status"] == "COMPLETED":
+                avg = res["avg_rewards"]
+                hist = res["metrics_history"]
+                ups = hist.get("policy_updates", [])
+                row.update(final_reward=round(float(avg[-1]), 4),
+                           max_reward=round(float(max(avg)), 4),
+                           evals=[round(float(x), 2) for x in hist.get("eval_rewards", [])],
+                           eval_episodes=[int(x) for x in hist.get("eval_episode_numbers", [])],
+                           env_steps=int(sum(u.get("steps", 0) for u in ups)),
+                           updates=len(ups),
+                           # the group's (or batch's) wall clock, shared by its experiments
+                           wall_s=round(wall, 1), train_s=round(wall, 1))
+                if e.seed in ref:
+                    row.update(reference_final_reward=ref[e.seed],
+                               delta=round(row["final_reward"] - ref[e.seed], 4))
+                if e.seed in solo:
+                    row["solo_r4_final_reward"] = solo[e.seed]
+                    same.append(row["final_reward"] == solo[e.seed])
+            else:
+                row["error"] = res.get("error_message")
+            rows.append(row)
+            f.write(json.dumps(row) + "\n")
+    done = [r["final_reward"] for r in rows if "final_reward" in r]
+    return {"wall_s": round(wall, 1), "n": len(done),
+            "mean_final_reward": round(sum(done) / len(done), 4) if done else None,
+            "equal_to_solo_r4": f"{sum(same)}/{len(same)}" if same else None,
+            "env_steps": int(sum(r.get("env_steps", 0) for r in rows)),
+            "cells_in_batch": unit_cells}
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--out", default="gpurun_out/sweep_reward")
@@ -52,6 +106,9 @@ def main():
     p.add_argument("--rollout", type=int, default=128)
     p.add_argument("--minibatches", type=int, default=32)
     p.add_argument("--eval-interval", type=int, default=50)
+    p.add_argument("--batch", action="store_true",
+                   help="run the cells of one hidden width as one ExperimentRunner.launch_batch "
+                        "(one GroupBatch: shared acting, env and minibatch-step launches)")
     args = p.parse_args()
     out = os.path.abspath(args.out)
     os.makedirs(out, exist_ok=True)
@@ -69,6 +126,7 @@ def main():
                          "eval_interval": args.eval_interval, "seeds": args.seeds},
               "cells": {}}
     t_all = time.time()
+    cell_exps = {}
     for cell in args.cells:
         cname, H = CELLS[cell]
         d_embed = None if cname == "sorted" else 4
@@ -87,65 +145,33 @@ def main():
             exps.append(Experiment(name=name, condition=conds[cname], hp=hp, seed=seed,
                                    max_episodes=args.episodes, target_reward=130.0, extra=extra,
                                    env_config_overrides={}))
-        run_dir = os.path.join(out, f"{cname}_h{H}_e{E}_t{T}")  # tools/condition_order.py layout
-        os.makedirs(run_dir, exist_ok=True)
-        work_dir = (run_dir if args.work is None
-                    else os.path.join(os.path.abspath(args.work), os.path.basename(run_dir)))
+        cell_exps[cell] = exps
+    # execution units: one launch_group per cell, or (--batch) one launch_batch per hidden width
+    if args.batch:
+        by_h = {}
+        for cell in args.cells:
+            by_h.setdefault(CELLS[cell][1], []).append(cell)
+        units = list(by_h.values())
+    else:
+        units = [[cell] for cell in args.cells]
+    for unit in units:
+        tag = unit[0] if len(unit) == 1 else "batch_h%d" % CELLS[unit[0]][1]
+        work_dir = os.path.join(os.path.abspath(args.work) if args.work else out, tag)
         os.makedirs(work_dir, exist_ok=True)
         cwd = os.getcwd()
         os.chdir(work_dir)
         t0 = time.time()
         try:
-            results = ExperimentRunner(HIGHWAY_CONFIG).launch_group(exps)
+            runner = ExperimentRunner(HIGHWAY_CONFIG)
+            per_cell = (runner.launch_batch([cell_exps[c] for c in unit]) if len(unit) > 1
+                        else [runner.launch_group(cell_exps[unit[0]])])
         finally:
             os.chdir(cwd)
         wall = time.time() - t0
-        solo = {}
-        solo_path = os.path.join(ROOT, "profiles", "r4", "reward", f"{cell}_e{E}_t{T}",
-                                 "summary.jsonl")
-        if os.path.exists(solo_path):
-            for line in open(solo_path):
-                r = json.loads(line)
-                if r.get("episodes") == args.episodes and r.get("eval_interval") == args.eval_interval:
-                    solo[int(r["seed"])] = r.get("final_reward")
-        rows, same = [], []
-        ref = reference_final(cname, H)
-        with open(os.path.join(run_dir, "summary.jsonl"), "w") as f:
-            for e, res in zip(exps, results):
-                row = {"condition": cname, "seed": e.seed, "experiment": e.name,
-                       "status": res["status"], "num_envs": E, "episodes": args.episodes,
-                       "rollout": T, "minibatches": M, "eval_interval": args.eval_interval,
-                       "lr": 3e-4, "epochs": 8, "hidden_dim": H, "obs_vehicles": 15,
-                       "order": "make_env default", "d_embed": d_embed, "grouped": len(exps)}
-                if res["status"] == "COMPLETED":
-                    avg = res["avg_rewards"]
-                    hist = res["metrics_history"]
-                    ups = hist.get("policy_updates", [])
-                    row.update(final_reward=round(float(avg[-1]), 4),
-                               max_reward=round(float(max(avg)), 4),
-                               evals=[round(float(x), 2) for x in hist.get("eval_rewards", [])],
-                               eval_episodes=[int(x) for x in hist.get("eval_episode_numbers", [])],
-                               env_steps=int(sum(u.get("steps", 0) for u in ups)),
-                               updates=len(ups),
-                               # the group's wall clock, shared by its experiments
-                               wall_s=round(wall, 1), train_s=round(wall, 1))
-                    if e.seed in ref:
-                        row.update(reference_final_reward=ref[e.seed],
-                                   delta=round(row["final_reward"] - ref[e.seed], 4))
-                    if e.seed in solo:
-                        row["solo_r4_final_reward"] = solo[e.seed]
-                        same.append(row["final_reward"] == solo[e.seed])
-                else:
-                    row["error"] = res.get("error_message")
-                rows.append(row)
-                f.write(json.dumps(row) + "\n")
-        done = [r["final_reward"] for r in rows if "final_reward" in r]
-        cell_rep = {"wall_s": round(wall, 1), "n": len(done),
-                    "mean_final_reward": round(sum(done) / len(done), 4) if done else None,
-                    "equal_to_solo_r4": f"{sum(same)}/{len(same)}" if same else None,
-                    "env_steps": int(sum(r.get("env_steps", 0) for r in rows))}
-        report["cells"][cell] = cell_rep
-        print(json.dumps({"cell": cell, **cell_rep}), flush=True)
+        for cell, results in zip(unit, per_cell):
+            report["cells"][cell] = _write_cell(out, cell, cell_exps[cell], results, wall,
+                                                len(unit), E, T, M, args, reference_final)
+            print(json.dumps({"cell": cell, **report["cells"][cell]}), flush=True)
     report["wall_s"] = round(time.time() - t_all, 1)
     with open(os.path.join(out, "sweep.json"), "w") as f:
         json.dump(report, f, indent=1)
