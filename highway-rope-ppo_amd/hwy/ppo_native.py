@@ -109,9 +109,26 @@ def flat_params(agent):
     hwy_ppo_param_layout order, created once per agent and shared by FusedPPO and fused_act."""
     cached = getattr(agent, "_flat", None)
     ac = agent.actor_critic
+    # fast path (every acting call lands here): the same module objects still hold the same
+    # parameters, still viewing the flat buffer -- checked through the modules' own dicts, not
+    # named_parameters(), whose module walk cost ~50 us per call
+    guard = getattr(agent, "_flat_guard", None)
+    if cached is not None and guard is not None and guard[0] is ac:
+        ok = True
+        for steps, p, ptr in guard[1]:
+            for d, k, obj in steps:
+                if d.get(k) is not obj:
+                    ok = False
+                    break
+            if not ok or p.data.data_ptr() != ptr:
+                ok = False
+                break
+        if ok:
+            return cached
     named = dict(ac.named_parameters())
     if cached is not None and all(named[n].data.data_ptr() == cached[0][o:].data_ptr()
                                   for n, o in zip(_PARAM_ORDER, cached[2])):
+        agent._flat_guard = _flat_guard(ac, cached[0], cached[2])
         return cached
     if set(named.keys()) != set(_PARAM_ORDER):
         raise ValueError("unexpected ActorCritic parameter layout for the fused step")
@@ -133,8 +150,26 @@ def flat_params(agent):
             p.grad = grads[off:off + n].view_as(p)
             params.append(p)
     agent._flat = (flat, grads, offs, params)
+    agent._flat_guard = _flat_guard(ac, flat, offs)
     agent._learners = {}  # a torch-graph learner captured the old storage
     return agent._flat
+
+
+def _flat_guard(ac, flat: torch.Tensor, offs) -> tuple:
+    """flat_params' fast-path check: per parameter the chain of (module dict, key, object) from
+    the ActorCritic down to it, the Parameter, and the flat-buffer address it must view."""
+    out = []
+    for name, off in zip(_PARAM_ORDER, offs):
+        parts = name.split(".")
+        steps, mod = [], ac
+        for part in parts[:-1]:
+            child = mod._modules[part]
+            steps.append((mod._modules, part, child))
+            mod = child
+        p = mod._parameters[parts[-1]]
+        steps.append((mod._parameters, parts[-1], p))
+        out.append((tuple(steps), p, flat[off:].data_ptr()))
+    return (ac, tuple(out))
 
 
 def _param_versions(agent, flat: torch.Tensor, params) -> tuple:
