@@ -125,6 +125,96 @@ def _run_eval_vector(env, agent, num_episodes, exp_seed):
     return float(total.mean().item())
 
 
+def evaluate_many(items, num_episodes=5):
+    """evaluate(env, agent, num_episodes, exp_seed) for every (env, agent, exp_seed) of `items`,
+    each result exactly what evaluate returns for it alone: the evaluations that are not memoised
+    run together, one grouped acting launch (hwy_ppo_group_act) and one grouped env launch
+    (hwy_step_group) per step over all their evaluation envs, the same kernels and the same
+    per-episode float64 sums as the solo loop.  Falls back to one evaluate per item where the
+    items cannot share launches (torch acting, mixed hidden widths, single items)."""
+    out = [None] * len(items)
+    todo = []
+    for i, (env, agent, seed) in enumerate(items):
+        key = _eval_key(agent, num_episodes, seed)
+        memo = getattr(env.unwrapped, "_eval_memo", None)
+        if memo is not None and memo[0] == key and key[0] is not None:
+            out[i] = memo[1]
+        else:
+            todo.append(i)
+    groups = {}
+    for i in todo:
+        env, agent, _ = items[i]
+        ok = (_is_vector(env) and getattr(agent, "backend", "torch") != "torch"
+              and agent.device.type == "cuda")
+        H = agent.actor_critic.shared[0].weight.shape[0] if ok else None
+        groups.setdefault(H, []).append(i)
+    for H, idx in groups.items():
+        if H is None or len(idx) < 2:
+            for i in idx:
+                out[i] = evaluate(items[i][0], items[i][1], num_episodes=num_episodes,
+                                  exp_seed=items[i][2])
+            continue
+        res = _run_eval_group([items[i] for i in idx], num_episodes)
+        for i, r in zip(idx, res):
+            env, agent, seed = items[i]
+            env.unwrapped._eval_memo = (_eval_key(agent, num_episodes, seed), r)
+            out[i] = r
+    return out
+
+
+def _run_eval_group(items, num_episodes):
+    """_run_eval_vector for several experiments in lockstep (evaluate_many)."""
+    from hwy.ppo_native import GroupAct
+    from hwy.vec_env import GroupEnvStep
+
+    evs, rows = [], []
+    n, k = num_episodes, len(items)
+    agents = [a for _, a, _ in items]
+    for env, agent, seed in items:
+        cache = getattr(env.unwrapped, "_eval_envs", None)
+        if cache is None:
+            cache = {}
+            env.unwrapped._eval_envs = cache
+        ev = cache.get(n)
+        if ev is None:
+            ev = cache[n] = _eval_env_like(env, n)
+        evs.append(ev)
+    dev = evs[0].device
+    act = GroupAct(agents, n)
+    tiles = act.tiles()
+    if any((t is None) != (tiles[0] is None) for t in tiles):  # one acting kernel per launch
+        return [_run_eval_vector(env, agent, n, seed) for env, agent, seed in items]
+    rew = torch.empty(k * n, device=dev)
+    te = torch.empty(k * n, dtype=torch.uint8, device=dev)
+    tr = torch.empty(k * n, dtype=torch.uint8, device=dev)
+    ios, keep = [], []  # keep: the act outputs the kernels write through raw addresses
+    for j, ((env, agent, seed), ev) in enumerate(zip(items, evs)):
+        seeds = torch.arange(n, device=dev, dtype=torch.int64) + (seed + 1000)
+        obs, _ = ev.reset(seeds=seeds)  # the eval handle's obs_buf, read and rewritten in place
+        a = torch.empty(n, 2, device=dev)
+        pre = torch.empty(n, 2, device=dev)
+        lp = torch.empty(n, device=dev)
+        val = torch.empty(n, device=dev)
+        sl = slice(j * n, (j + 1) * n)
+        keep.append((a, pre, lp, val))
+        rows.append((obs.data_ptr(), None, a.data_ptr(), pre.data_ptr(), lp.data_ptr(),
+                     val.data_ptr()))
+        ios.append((a, obs, rew[sl], te[sl], tr[sl], None, None))
+    step = GroupEnvStep(evs)
+    alive = torch.ones(k * n, dtype=torch.bool, device=dev)
+    total = torch.zeros(k * n, dtype=torch.float64, device=dev)
+    for s_ in range(max(ev.max_episode_steps for ev in evs) + 1):
+        act.launch(rows, tiles)
+        step.launch(ios)
+        total += torch.where(alive, rew.double(), torch.zeros_like(total))
+        alive &= ~(te.bool() | tr.bool())
+        if s_ % 8 == 7 and not bool(alive.any()):
+            break
+    res = [float(total[j * n:(j + 1) * n].mean().item()) for j in range(k)]
+    del keep
+    return res
+
+
 # ---------------------------------------------------------------------------------- artifacts
 def _save_artifacts(artifacts_dir, checkpoint_dir, experiment_name, metrics_history,
                     training_episodes, episode_rewards, eval_episodes, rewards, avg_rewards,
@@ -180,8 +270,9 @@ class _EvalTracker:
         self.best = -float("inf")
         self.solved = False
 
-    def initial(self):
-        r = evaluate(self.env, self.agent, num_episodes=5, exp_seed=self.exp_seed)
+    def initial(self, r=None):
+        if r is None:
+            r = evaluate(self.env, self.agent, num_episodes=5, exp_seed=self.exp_seed)
         self.rewards.append(r)
         self.avg_rewards.append(r)
         self.mh["eval_rewards"].append(r)
@@ -190,9 +281,11 @@ class _EvalTracker:
         self.mh["timestamps"].append(0)
         self.logger.info(f"{self.prefix} initial_eval reward={r:.2f}")
 
-    def on_episode(self, episode_num):
+    def on_episode(self, episode_num, r=None):
+        """r: the evaluation's result when the caller ran it (evaluate_many), else evaluated here."""
         self.logger.info(f"{self.prefix} Evaluating at episode {episode_num}...")
-        r = evaluate(self.env, self.agent, num_episodes=5, exp_seed=self.exp_seed)
+        if r is None:
+            r = evaluate(self.env, self.agent, num_episodes=5, exp_seed=self.exp_seed)
         self.rewards.append(r)
         self.eval_episodes.append(episode_num)
         elapsed = time.time() - self.t0
@@ -400,11 +493,16 @@ def train_batch(stepper, groups, experiment_names, exp_seeds, max_episodes=500, 
         tracker = _EvalTracker(grp.solo_envs[j], grp.agents[j], int(exp_seeds[k]),
                                target_reward, checkpoint_dir, name, mh, logger, prefix, start_time)
         logger.info(f"{prefix} Performing initial evaluation...")
-        tracker.initial()
         runs.append({"name": name, "logger": logger, "prefix": prefix, "mh": mh,
                      "tracker": tracker, "episode_rewards": [], "training_episodes": [],
                      "episode_num": 0, "total_steps": 0, "done": max_episodes <= 0,
-                     "group": grp, "j": j})
+                     "group": grp, "j": j, "pending": []})
+    # every experiment's evaluations run together (evaluate_many: the same results as one
+    # evaluate each -- deterministic episodes, no random numbers drawn)
+    first = evaluate_many([(r["tracker"].env, r["tracker"].agent, r["tracker"].exp_seed)
+                           for r in runs])
+    for r, v in zip(runs, first):
+        r["tracker"].initial(v)
     while not all(r["done"] for r in runs):
         t_update = time.time()
         stepper.rollout()
@@ -430,11 +528,22 @@ def train_batch(stepper, groups, experiment_names, exp_seeds, max_episodes=500, 
                 _log_episode(r["logger"], r["prefix"], r["episode_num"], ret, r["episode_rewards"],
                              log_interval, r["total_steps"], start_time)
                 if r["episode_num"] % eval_interval == 0:
-                    r["tracker"].on_episode(r["episode_num"])
+                    r["pending"].append(r["episode_num"])
             r["mh"]["policy_updates"].append({"episode": r["episode_num"], "steps": T * E,
                                               "time": time.time() - t_update, **upd})
             if r["episode_num"] >= max_episodes:
                 r["done"] = True
+        # this iteration's evaluations (weights unchanged since its update): one per experiment
+        # that crossed an evaluation point, all together; a second point in the same iteration
+        # evaluates the same weights and gets the same (memoised) value
+        due = [r for r in runs if r["pending"]]
+        if due:
+            vals = evaluate_many([(r["tracker"].env, r["tracker"].agent, r["tracker"].exp_seed)
+                                  for r in due])
+            for r, v in zip(due, vals):
+                for ep in r["pending"]:
+                    r["tracker"].on_episode(ep, v)
+                r["pending"] = []
     out = []
     for r in runs:
         tr = r["tracker"]
