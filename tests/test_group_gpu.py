@@ -315,3 +315,38 @@ def test_runner_launch_batch_equals_launch_group(tmp_path, monkeypatch):
             assert ma["episode_rewards"] == mb["episode_rewards"]
             assert [u["loss"] for u in ma["policy_updates"]] == \
                 [u["loss"] for u in mb["policy_updates"]]
+
+
+@pytest.mark.parametrize("E", [4096, 16384])
+def test_parameter_table_step_equals_hwy_step_at_rollout_sizes(E):
+    """The lockstep rollout's env launch (hwy_step_group over its one handle: the launch
+    parameters read from a device table) against hwy_step's by-value kernel on a twin handle, at
+    the default line's 4,096 envs (4-wave build) and at 16,384 (6-wave build, more envs than
+    four waves per SIMD): the same observations, rewards, flags and episode statistics."""
+    from config.base_config import HIGHWAY_CONFIG
+    from hwy.vec_env import GroupEnvStep, HighwayVecEnv
+
+    envs = [HighwayVecEnv(HIGHWAY_CONFIG, num_envs=E, device=DEV, autoreset=True, seed_base=42)
+            for _ in range(2)]
+    for env in envs:
+        env.reset()
+
+    def bufs():
+        return (torch.empty(E, 2, device=DEV), torch.empty_like(envs[0].obs_buf),
+                torch.empty(E, device=DEV), torch.empty(E, dtype=torch.uint8, device=DEV),
+                torch.empty(E, dtype=torch.uint8, device=DEV), torch.empty(E, device=DEV),
+                torch.empty(E, dtype=torch.int32, device=DEV))
+
+    a, b = bufs(), bufs()
+    g = GroupEnvStep([envs[1]])
+    gen = torch.Generator(device=DEV).manual_seed(11)
+    for step in range(24):
+        a[0].copy_(torch.rand(E, 2, device=DEV, generator=gen) * 2 - 1)
+        b[0].copy_(a[0])
+        envs[0].step_into(*a)
+        g.launch([b])
+        torch.cuda.synchronize()
+        for k in range(1, 7):
+            assert torch.equal(a[k], b[k]), (step, k)
+    for env in envs:
+        env.close()
