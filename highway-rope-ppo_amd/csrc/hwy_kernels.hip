@@ -1232,7 +1232,8 @@ __device__ void frame_wave(const hwy_config& C, int lane, Veh& v, float dt, floa
 // env on 4 waves per SIMD (4,096 envs on 256 CUs: 0.160 ms); 6 (80 VGPRs, 14 spilled to scratch
 // outside the hot loop) when more envs queue behind them: 16,384 envs 0.412 -> 0.365 ms,
 // 32,768 0.775 -> 0.670 (5 waves: 0.381 / 0.702), 8,192 0.228 -> 0.220; at 4,096 envs the 6-wave
-// build takes 0.164 ms, so hwy_launch_step picks by env count
+// build takes 0.164 ms, so hwy_launch_step picks by env count (round 6, launch parameters from a
+// table: the 4-wave build also wins at 8,192 envs, so the 6-wave one starts above 32 envs per CU)
 // The step of one handle's envs; the kernels below run it for one handle (hwy_step) or for
 // handle blockIdx.y of a table (hwy_step_group: a sweep's cells in one launch).  It reads no
 // gridDim and no blockIdx.y, so a grouped launch computes every env exactly as its handle's own.
@@ -1501,7 +1502,16 @@ __global__ void hwy_math_kernel(int op, const float* in, const float* in2, float
 extern "C" {
 // compute units of the current device (cached per device; 256 without one)
 // waves per SIMD the step kernel's registers are sized for at large E (5 and 8 measured slower)
-constexpr int kStepBigW = 6;
+#ifndef HWY_STEP_BIG_W
+#define HWY_STEP_BIG_W 6
+#endif
+// envs per CU above which the big build runs: at 8,192 envs (32 per CU) the 4-wave build is
+// 6-7 % faster than the 6-wave one (0.205 vs 0.219-0.245 ms per step), at 16,384 the 6-wave build
+// wins (0.295 vs 0.324) and at 32,768 ties the 5-wave one (profiles/r6/micro/ab_bigw.log)
+#ifndef HWY_STEP_BIG_WAVES
+#define HWY_STEP_BIG_WAVES 32
+#endif
+constexpr int kStepBigW = HWY_STEP_BIG_W;
 static int device_cus() {
   static int cache[64] = {};
   int dev = 0;
@@ -1523,7 +1533,7 @@ static int device_cus() {
 int hwy_launch_step(const StepParams* p, hipStream_t s) {
   const int blocks = (p->cfg.num_envs + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
   // one wave per env: more than 4 waves per SIMD of envs queue behind the first four
-  if ((int64_t)p->cfg.num_envs > (int64_t)16 * device_cus())
+  if (hwy_step_big(p->cfg.num_envs))
     hipLaunchKernelGGL(hwy_step_kernel<kStepBigW>, dim3(blocks), dim3(ENVS_PER_BLOCK * WAVE), 0, s, *p);
   else
     hipLaunchKernelGGL(hwy_step_kernel<4>, dim3(blocks), dim3(ENVS_PER_BLOCK * WAVE), 0, s, *p);
@@ -1539,7 +1549,9 @@ int hwy_launch_step_group(const StepParams* dtab, int n, int blocks, int big, hi
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int hwy_step_blocks(int num_envs) { return (num_envs + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK; }
-int hwy_step_big(int64_t total_envs) { return total_envs > (int64_t)16 * device_cus() ? 1 : 0; }
+int hwy_step_big(int64_t total_envs) {
+  return total_envs > (int64_t)HWY_STEP_BIG_WAVES * device_cus() ? 1 : 0;
+}
 int hwy_launch_reset(const StepParams* p, hipStream_t s) {
   const int blocks = (p->cfg.num_envs + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
   hipLaunchKernelGGL(hwy_reset_kernel, dim3(blocks), dim3(ENVS_PER_BLOCK * WAVE), 0, s, *p);
